@@ -1,0 +1,44 @@
+# Build of the product library (libzrt.so: HIP kernels for gfx950 + host C++)
+# and the drop-in CLI.  Everything lands in-tree so it travels to the GPU box.
+ROCM      ?= /opt/rocm
+HIPCC     := $(ROCM)/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+PKG       := zig_raytracing_contest_amd
+SRC       := $(PKG)/csrc
+OBJ       := build/obj
+# -ffp-contract=off everywhere: the reference (Zig) never contracts a*b+c.
+HIPFLAGS  := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+             -Wall -Wno-unused-function -Iinclude
+CXXFLAGS  := -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Iinclude -pthread
+HDRS      := include/zrt.h $(SRC)/zrt_math.h $(SRC)/zrt_internal.h
+HOST_SRCS := $(filter-out $(SRC)/cli.cpp,$(wildcard $(SRC)/*.cpp))
+HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(HOST_SRCS))
+LIB       := $(PKG)/libzrt.so
+CLI       := $(PKG)/bin/zrt
+
+all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) oracle
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) $(wildcard $(SRC)/*.h)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/render.o: $(SRC)/render.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)/render.o $(HOST_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lz -pthread
+
+$(CLI): $(SRC)/cli.cpp $(LIB) include/zrt.h
+	@mkdir -p $(PKG)/bin
+	$(CXX) $(CXXFLAGS) -o $@ $(SRC)/cli.cpp -L$(PKG) -lzrt -Wl,-rpath,'$$ORIGIN/..' -Wl,-rpath,$(ROCM)/lib
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIB) $(PKG)/bin
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all clean oracle

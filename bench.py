@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s of the render hot path on the contest config.
+
+BASELINE.json metric "Mrays/sec + wall-clock to output.png on contest
+config.json scene", configs[2]: contest scene, 1920x1080, 256 spp, 1 MI355X.
+The contest round1.gltf is not in the container, so the scene is the
+deterministic ~100k-triangle stand-in of zig_raytracing_contest_amd/scenes.py
+("Camera 1", aspect 16:9, --height 1080), config.json max_bounce 4, grid 128^3.
+
+A step = one full render of that frame (530,841,600 path samples) on the
+device-resident scene: path-trace kernel + in-order sample resolve + RGB8, and
+for N > 1 the RCCL gather of every rank's packed RGB8 tiles to rank 0.
+Mrays = Scene.traceRay segments (primary + bounce + pass-through).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Image tiles (64x64, interleaved t % N) shard the
+frame: total work is fixed as N grows ("scaling": "strong").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic bytes: 8 B per visited Cell, 36 B per triangle
+# test (v0, e1, e2 as 9 f32), per hit 64 B of Triangle.Data + 4 texels x
+# (12 B base colour + 12 B emissive + 4 B transparency), 3 B per output pixel.
+B_CELL, B_TRI, B_HIT, B_PIX = 8, 36, 64 + 4 * (12 + 12 + 4), 3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg3", choices=sorted(scenes.CONFIGS))
+    ap.add_argument("--spp", type=int, default=None, help="override spp (NOT the headline)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(soup, cfg, target_s):
+    """Oracle in REF mode (the reference's Xoshiro-per-thread, contiguous
+    blocks, recursion) on a bounded, evenly spread sample of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc   # test infrastructure: the CPU baseline leg only
+    c = soup.camera(cfg["camera"])
+    cam = orc.camera_from_matrix(c.matrix, c.yfov, c.aspect, cfg["width"], cfg["height"])
+    osc = orc.OracleScene(soup)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16,
+                         len(os.sched_getaffinity(0))))
+    npx = cam.w * cam.h
+    spp = 4
+
+    def run(stride):
+        pixels = np.arange(0, npx, stride, dtype=np.uint32)
+        t0 = time.perf_counter()
+        _, _, ctr = osc.render_pixels(cam, spp, cfg["max_bounce"], pixels, orc.RNG_REF, 0, threads)
+        return time.perf_counter() - t0, ctr, pixels.size
+
+    dt, ctr, n = run(4096)                      # calibration
+    rate = max(ctr[0], 1) / max(dt, 1e-3)
+    want = rate * target_s                      # segments in ~target_s
+    seg_per_px = max(float(ctr[0]) / n, 1.0)
+    stride = max(1, int(npx / max(want / seg_per_px, 1.0)))
+    dt, ctr, n = run(stride)
+    return {"value": round(float(ctr[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} pixels (every {stride}th of {cam.w}x{cam.h}) x {spp} spp, "
+                      f"{int(ctr[0])} segments in {dt:.1f}s; oracle REF mode (Xoshiro256++ per "
+                      f"thread, contiguous blocks, recursion), gcc -O2, {threads} threads"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfgd = dict(scenes.CONFIGS[a.config])
+    spp = a.spp or cfgd["spp"]
+    soup = scenes.get_scene(cfgd["scene"])
+    cam = camera_for(soup, cfgd["camera"], cfgd["width"], cfgd["height"])
+    rs = RenderScene(soup, device=local)
+    P = native.tile_pixels(cam.w, cam.h, 64, rank, world).size
+
+    torch = None
+    dev_buf = None
+    gather_bufs = None
+    if world > 1:
+        import torch
+        maxP = max(native.tile_pixels(cam.w, cam.h, 64, r, world).size for r in range(world))
+        dev_buf = torch.zeros(maxP * 3, dtype=torch.uint8, device=f"cuda:{local}")
+        gather_bufs = [torch.zeros_like(dev_buf) for _ in range(world)] if rank == 0 else None
+
+    def step(stats=False):
+        ptr = dev_buf.data_ptr() if dev_buf is not None else None
+        res = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world,
+                                stats=stats, device_ptr=ptr)
+        if world > 1:
+            torch.cuda.synchronize()
+            dist.gather(dev_buf, gather_bufs, dst=0)
+        return res["stats"]
+
+    # untimed counting run: exact algorithmic work of one step (same RNG ->
+    # same paths as the timed kernel)
+    cst = step(stats=True)
+    for _ in range(a.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    kern_ms, launches, segs = 0.0, 0, 0
+    for _ in range(a.steps):
+        st = step()
+        kern_ms += st["trace_kernel_ms"]
+        launches += st["trace_launches"]
+        segs += st["segments"]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, total_segs = float(tmax[0]), float(t[1])
+    else:
+        total_segs = float(segs)
+
+    if rank == 0:
+        assert cst["segments"] * a.steps == segs, "counting and timed kernels disagree"
+        avg_launch_s = kern_ms / 1e3 / max(launches, 1)
+        alg_bytes = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] +
+                     B_HIT * cst["hits"] + B_PIX * P)
+        per_launch = alg_bytes / max(cst["trace_launches"], 1)
+        achieved = per_launch / avg_launch_s / 1e9
+        out = {
+            "metric": "Mrays/sec + wall-clock to output.png on contest config.json scene",
+            "value": round(total_segs / elapsed / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{a.config}: {cfgd['scene']} stand-in "
+                                   f"({soup.num_triangles} tris, {rs.geometry.num_refs} refs), "
+                                   f"{cam.w}x{cam.h}, {spp} spp, max_bounce "
+                                   f"{cfgd['max_bounce']}, grid 128^3",
+                       "global_batch": cam.w * cam.h * spp, "parallelism": f"tiles{world}",
+                       "segments_per_step": int(total_segs / a.steps)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                         "traffic": None,
+                         "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "alg_bytes_per_launch": int(per_launch)},
+            "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
+                                               "hits", "samples")},
+        }
+        if not a.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(soup, cfgd, a.cpu_seconds)
+            out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    rs.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

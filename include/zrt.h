@@ -1,0 +1,211 @@
+/*
+ * zrt.h -- C ABI of the MI355X-native render hot path (libzrt.so).
+ *
+ * Drop-in boundary for the reference's render seam
+ *     pub fn render(self: Scene, threads: []std.Thread, camera: Camera,
+ *                   img: []RGB) !void                  (src/stage3.zig:247)
+ * called once from src/main.zig:126.  The reference has no plugin registry;
+ * its only FFI mechanism is @cImport of C headers (src/c.zig:1-5) plus a
+ * static C library linked by build.zig:29-48, so a Zig host binds this
+ * header the same way.
+ *
+ * Zig's @Vector(3, f32) (16-byte padded) and std.MultiArrayList are not
+ * C-ABI, so the Scene is passed FLATTENED: plain pointers and sizes, caller
+ * owned, read-only for the duration of the call.  All functions are
+ * synchronous, return 0 (ZRT_OK) or a negative zrt_status, and never throw.
+ * No torch types appear anywhere in this interface.
+ */
+#ifndef ZRT_H
+#define ZRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZRT_ABI_VERSION 1
+
+typedef enum zrt_status {
+    ZRT_OK = 0,
+    ZRT_ERR_INVALID_ARG = -1,     /* null pointer, zero size, inconsistent scene */
+    ZRT_ERR_NO_DEVICE = -2,       /* no HIP device / bad ordinal */
+    ZRT_ERR_HIP = -3,             /* a HIP runtime call failed */
+    ZRT_ERR_OUT_OF_MEMORY = -4,   /* host or device allocation failed */
+    ZRT_ERR_UNSUPPORTED = -5,     /* e.g. max_bounce above the compiled stack depth */
+    ZRT_ERR_IO = -6,              /* file open/read/write failed */
+    ZRT_ERR_PARSE = -7,           /* glTF / JSON / PNG malformed */
+    ZRT_ERR_NOT_FOUND = -8,       /* camera name not found, no cameras (stage1.zig:282-307) */
+    ZRT_ERR_CAMERA = -9,          /* stage1.zig:322-342 width/height/aspect-ratio rules */
+} zrt_status;
+
+/* ---- scene (stage3.zig:136-143 Scene, flattened) ------------------------ */
+
+/* linalg.zig:407-410 Grid */
+typedef struct zrt_grid {
+    float bbox_min[3];
+    float bbox_max[3];
+    uint32_t resolution[3];
+    float cell_size[3];              /* (bbox_max - bbox_min) / resolution, f32 */
+} zrt_grid;
+
+/* stage3.zig:82-92 Texture(T).  `offset` indexes zrt_scene.texels in floats;
+ * colour textures hold 3 floats per texel (linear RGB, factor applied),
+ * transparency textures 1 float per texel.  Rows top to bottom.
+ * u/v_min/max: [0, w-1] for CLAMP_TO_EDGE, [INT32_MIN, INT32_MAX] for repeat
+ * (stage1.zig:381-409); a missing texture is a 1x1 texel = factor
+ * (stage1.zig:411-425). */
+typedef struct zrt_texture {
+    uint64_t offset;
+    int32_t w, h;
+    int32_t u_min, u_max, v_min, v_max;
+    int32_t _pad;
+} zrt_texture;
+
+/* stage3.zig:125-129 Material */
+typedef struct zrt_material {
+    zrt_texture base_color;          /* 3 floats/texel */
+    zrt_texture emissive;            /* 3 floats/texel */
+    zrt_texture transparency;        /* 1 float/texel  */
+} zrt_material;
+
+typedef struct zrt_scene {
+    zrt_grid grid;
+    uint32_t num_cells;              /* resolution[0]*resolution[1]*resolution[2] */
+    const uint32_t* cells;           /* num_cells * {begin, end}   (stage3.zig:131-134) */
+    uint32_t num_triangles;          /* baked refs: cell order, duplicated (stage2.zig:137-164) */
+    const float* triangles_pos;      /* num_triangles * 9: v0, e1 = v1-v0, e2 = v2-v0 (linalg.zig:683-694) */
+    const float* triangles_data;     /* num_triangles * 15: normal[3] x3, texcoord[2] x3 (stage3.zig:44-51) */
+    const uint32_t* triangles_material; /* num_triangles (Data.material_idx) */
+    uint32_t num_materials;
+    const zrt_material* materials;
+    const float* texels;
+    uint64_t num_texel_floats;
+} zrt_scene;
+
+/* stage3.zig:19-26 Camera (built by stage1.zig:309-371) */
+typedef struct zrt_camera {
+    uint32_t w, h;
+    float origin[3];
+    float lower_left_corner[3];
+    float right[3];
+    float up[3];                     /* points world-down: row 0 is the top image row */
+} zrt_camera;
+
+/* main.zig:56-61 Config (num_samples/max_bounce) + device-side knobs that
+ * the reference's config.json does not have (kept out of config.json). */
+typedef struct zrt_render_config {
+    uint32_t num_samples;            /* spp, 1..65535 (u16 in the reference) */
+    uint32_t max_bounce;             /* recursion depth of traceRayRecursive */
+    uint64_t seed;                   /* counter-RNG key (0 = default) */
+    int32_t device;                  /* HIP ordinal, -1 = current device */
+    uint32_t rank;                   /* this process's shard of the image */
+    uint32_t num_ranks;              /* tiles t with t % num_ranks == rank */
+    uint32_t tile_size;              /* square tile edge in pixels, 0 = 64 */
+    uint32_t flags;                  /* ZRT_FLAG_* */
+    uint32_t _reserved[5];
+} zrt_render_config;
+
+#define ZRT_FLAG_COUNT_STATS  0x1u   /* count cells/tests/hits (slower kernel variant) */
+
+/* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
+ * transparency pass-through); Mrays/s = segments / render time. */
+typedef struct zrt_stats {
+    uint64_t segments;
+    uint64_t cells_visited;          /* only with ZRT_FLAG_COUNT_STATS */
+    uint64_t triangle_tests;         /* only with ZRT_FLAG_COUNT_STATS */
+    uint64_t hits;                   /* only with ZRT_FLAG_COUNT_STATS */
+    uint64_t samples;                /* pixels x spp rendered by this call */
+    double render_ms;                /* device time: all kernels of the render */
+    double trace_kernel_ms;          /* device time: path-trace kernel launches only */
+    uint32_t trace_launches;
+    uint32_t _pad;
+} zrt_stats;
+
+const char* zrt_error_string(int status);
+int zrt_abi_version(void);
+int zrt_device_count(int* count);
+
+/* ---- stage 2: grid build + bake (stage2.zig:44-164) --------------------- */
+typedef struct zrt_geometry zrt_geometry;
+
+/* positions n*9 (v0,v1,v2 world space), normals n*9, texcoords n*6,
+ * material n.  Inputs are read during the call only.  Deterministic:
+ * identical to the single-threaded reference order (triangle order within
+ * a cell), whatever the host thread count. */
+int zrt_geometry_build(const float* positions, const float* normals, const float* texcoords,
+                       const uint32_t* material, uint32_t num_triangles,
+                       const uint32_t resolution[3], uint32_t num_threads, zrt_geometry** out);
+/* Fills grid/cells/triangle arrays of *scene (views into the geometry,
+ * valid until zrt_geometry_free); leaves the material fields untouched. */
+int zrt_geometry_scene(const zrt_geometry* g, zrt_scene* scene);
+/* Source triangle index of each baked ref (stage2 Geometry.indices). */
+int zrt_geometry_indices(const zrt_geometry* g, const uint32_t** indices, uint32_t* count);
+void zrt_geometry_free(zrt_geometry* g);
+
+/* ---- stage 3: the render seam ------------------------------------------ */
+
+/* One-shot drop-in for Scene.render: uploads the scene, renders the whole
+ * image (rank 0 of 1) on `cfg->device`, writes w*h*3 RGB8 into rgb_out
+ * (caller-allocated, row 0 = top), frees device memory, returns. */
+int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_render_config* cfg,
+               uint8_t* rgb_out, zrt_stats* stats);
+
+/* Device-resident path (scene uploaded once, many renders). */
+typedef struct zrt_context zrt_context;
+
+typedef struct zrt_outputs {
+    uint8_t* rgb_image;              /* host w*h*3; only this rank's pixels are written */
+    uint8_t* rgb_packed;             /* host n_owned*3 in zrt_tile_pixels order */
+    float* linear_packed;            /* host n_owned*3: pixel sum * (1/spp), pre-toRGB */
+    void* device_rgb_packed;         /* device n_owned*3 on the context's device */
+} zrt_outputs;
+
+int zrt_context_create(const zrt_scene* scene, int device, zrt_context** out);
+int zrt_context_render(zrt_context* ctx, const zrt_camera* camera, const zrt_render_config* cfg,
+                       const zrt_outputs* outputs, zrt_stats* stats);
+void zrt_context_destroy(zrt_context* ctx);
+
+/* Pixels owned by `rank` (row-major image indices) in the packed output
+ * order: tiles t = rank, rank+num_ranks, ... (row-major tile order), each
+ * tile walked in 8x8 blocks.  pixels may be NULL to query *count. */
+int zrt_tile_pixels(uint32_t w, uint32_t h, uint32_t tile_size, uint32_t rank,
+                    uint32_t num_ranks, uint32_t* pixels, uint32_t* count);
+
+/* ---- stage 1: glTF scene load + camera (stage1.zig) --------------------- */
+typedef struct zrt_gltf zrt_gltf;
+
+/* Loads .gltf (+ .bin, + PNG images) or .glb; triangle soup in node order
+ * (stage1.zig:217-259), materials (stage1.zig:381-496), cameras. */
+int zrt_gltf_load(const char* path, uint32_t num_threads, zrt_gltf** out);
+int zrt_gltf_soup(const zrt_gltf* g, const float** positions, const float** normals,
+                  const float** texcoords, const uint32_t** material, uint32_t* num_triangles);
+/* Fills the material/texel fields of *scene (views valid until free). */
+int zrt_gltf_materials(const zrt_gltf* g, zrt_scene* scene);
+/* stage1.zig:309-371; width/height < 0 mean "not given". */
+int zrt_gltf_camera(const zrt_gltf* g, const char* camera_name, int32_t width, int32_t height,
+                    zrt_camera* out);
+void zrt_gltf_free(zrt_gltf* g);
+
+/* stage1.zig:309-371 from an explicit node matrix (column-major 16). */
+int zrt_camera_from_matrix(const float matrix[16], float yfov, int has_aspect_ratio,
+                           float aspect_ratio, int32_t width, int32_t height, zrt_camera* out);
+
+/* ---- device-function parity probes (tests only; run on the GPU) -------- */
+enum {
+    ZRT_PROBE_TRIANGLE = 0,   /* in n*15 (v0,v1,v2,orig,dir) -> out n*4 (hit,t,u,v) */
+    ZRT_PROBE_BBOX = 1,       /* in n*12 (min,max,orig,dir) -> out n*2 (hit,t) */
+    ZRT_PROBE_DDA = 2,        /* in n*12 (min,max,orig,dir) + res in aux -> out n*(1+4*64) */
+    ZRT_PROBE_TO_RGB = 3,     /* in n*3 -> out n*3 (as float) */
+    ZRT_PROBE_RNG_F32 = 4,    /* in n*3 u32 (seed_lo,pixel,sample) -> out n*16 floats */
+    ZRT_PROBE_RNG_NORM = 5,   /* same -> out n*16 floats */
+    ZRT_PROBE_EXP_LOG = 6,    /* in n doubles -> out n*2 doubles (exp, log) */
+    ZRT_PROBE_TEXTURE = 7,    /* in n*2 (u,v) + aux texture -> out n*3 */
+};
+int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZRT_H */

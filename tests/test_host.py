@@ -1,0 +1,102 @@
+"""Host-side logic that runs without a GPU: camera rules, tile sharding,
+config.json, C-ABI exports."""
+import json
+import math
+import re
+
+import numpy as np
+import pytest
+
+from zig_raytracing_contest_amd import Config, camera_for, native, scenes
+
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+
+
+def test_abi_exports_every_declared_symbol():
+    hdr = open(f"{ROOT}/include/zrt.h").read()
+    declared = set(re.findall(r"\b(zrt_[a-z0-9_]+)\s*\(", hdr))
+    L = native.lib()
+    missing = [s for s in sorted(declared) if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.zrt_abi_version() == 1
+    assert L.zrt_error_string(-5) == b"unsupported configuration"
+
+
+@pytest.mark.parametrize("name,cam,w,h", [("sphere", None, 256, 256), ("cornell", None, 512, 512),
+                                          ("contest", "Camera 1", None, 1080),
+                                          ("contest", "Camera 2", 3840, None),
+                                          ("sponza", None, None, 1080)])
+def test_camera_matches_oracle(oracle_mod, name, cam, w, h):
+    soup = scenes.get_scene(name)
+    c = soup.camera(cam)
+    a = camera_for(soup, cam, w, h)
+    b = oracle_mod.camera_from_matrix(c.matrix, c.yfov, c.aspect, w, h)
+    assert (a.w, a.h) == (b.w, b.h)
+    for k1, k2 in (("origin", "origin"), ("lower_left_corner", "llc"), ("right", "right"),
+                   ("up", "up")):
+        assert list(getattr(a, k1)) == list(getattr(b, k2)), k1
+
+
+def test_camera_size_rules():
+    m = scenes.look_at((0, 0, 3), (0, 0, 0))
+    # stage1.zig:322-342
+    with pytest.raises(native.ZrtError):
+        native.camera_from_matrix(m, 0.8, None, None, None)       # OutputImgSizeIsNotSpecified
+    with pytest.raises(native.ZrtError):
+        native.camera_from_matrix(m, 0.8, 1.5, 100, 100)          # CameraHasAspectRatio
+    with pytest.raises(native.ZrtError):
+        native.camera_from_matrix(m, 0.8, None, 100, None)        # CameraHasntAspectRatio
+    c = native.camera_from_matrix(m, 0.8, 16 / 9, None, 1080)
+    assert (c.w, c.h) == (1920, 1080)
+    c = native.camera_from_matrix(m, 0.8, 16 / 9, 1920, None)
+    assert (c.w, c.h) == (1920, 1080)
+    # up points world-down so row 0 is the top image row
+    assert c.up[1] < 0
+
+
+@pytest.mark.parametrize("w,h,tile,n", [(256, 256, 64, 1), (1920, 1080, 64, 8), (100, 37, 16, 3),
+                                        (1, 1, 8, 2), (130, 70, 64, 5)])
+def test_tile_partition_is_exact(w, h, tile, n):
+    seen = np.zeros(w * h, np.int32)
+    for r in range(n):
+        px = native.tile_pixels(w, h, tile, r, n)
+        seen[px] += 1
+    assert (seen == 1).all()
+
+
+def test_tile_order_blocks_of_64():
+    px = native.tile_pixels(128, 128, 64, 0, 1)
+    # first wave = first 8x8 block of the first tile
+    blk = px[:64]
+    assert sorted(blk.tolist()) == sorted(y * 128 + x for y in range(8) for x in range(8))
+
+
+def test_config_json(tmp_path):
+    p = tmp_path / "config.json"
+    p.write_text(json.dumps({"grid_resolution": [128, 128, 128], "num_threads": None,
+                             "num_samples": 3, "max_bounce": 4}))
+    c = Config.load(str(p))
+    assert c.grid_resolution == (128, 128, 128) and c.num_threads is None
+    assert (c.num_samples, c.max_bounce) == (3, 4)
+    p.write_text(json.dumps({"grid_resolution": [1, 2, 3], "num_samples": 1, "max_bounce": 1,
+                             "bogus": 1}))
+    with pytest.raises(ValueError):
+        Config.load(str(p))
+
+
+def test_reference_config_json_parses():
+    ref = f"{ROOT}/config.json"
+    c = Config.load(ref)
+    assert c.grid_resolution == (128, 128, 128) and c.num_samples == 3 and c.max_bounce == 4
+
+
+def test_render_needs_gpu_and_fails_loudly():
+    if native.device_count() > 0:
+        pytest.skip("GPU present")
+    soup = scenes.get_scene("sphere")
+    g = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, (32, 32, 32))
+    keep = []
+    native.attach_materials(g.scene, soup.tex_desc, soup.texels, keep)
+    with pytest.raises(native.ZrtError) as e:
+        native.Context(g.scene)
+    assert e.value.status == -2

@@ -1,0 +1,831 @@
+// render.hip -- the render hot path on CDNA4 (gfx950): persistent path-trace
+// kernel + in-order sample resolve, behind the C ABI of include/zrt.h.
+//
+// Reference: Scene.render / renderWorker / traceRayRecursive / traceRay
+// (src/stage3.zig:152-256) over Grid.traceRay + Iterator.next
+// (src/linalg.zig:443-496) and Triangle.rayIntersection (linalg.zig:696-722).
+//
+// Work decomposition (MI355X-first, not the reference's thread blocks):
+//   * a work item is ONE path sample (pixel, sample); items are numbered
+//     sample-major over this rank's packed pixel list (64x64 tiles walked in
+//     8x8 blocks, so one wave64 = one 8x8 pixel block of one sample index:
+//     coherent primary rays);
+//   * a persistent grid (CUs x resident blocks) pulls 64-item chunks from one
+//     atomic counter per pass, one returning atomic per wave (dequeue row of
+//     the MI355X price list: far below the ~100 us a chunk takes);
+//   * each lane traces its path iteratively (recursion -> loop) and keeps the
+//     per-bounce (emissive, albedo) pairs in registers, folding them back to
+//     front at the end: e0 + a0*(e1 + a1*(...)) is the recursion's exact
+//     arithmetic, so the radiance is bit-identical to traceRayRecursive;
+//   * each sample radiance is written to HBM (float4, coalesced 1 KiB per wave
+//     instruction) and a resolve kernel sums a pixel's samples IN SAMPLE ORDER
+//     (renderWorker's `pixel = pixel.add(ray_color)`), scales by the f32
+//     reciprocal of spp and quantizes with toRGB.  The round trip costs
+//     32 B/sample of HBM traffic (~3 ms for cfg3's 531M samples at 6 TB/s)
+//     and buys order-independent scheduling with an exact result.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "zrt_internal.h"
+
+using namespace zrt;
+
+#define HIP_TRY(expr)                                                            \
+    do {                                                                         \
+        hipError_t _e = (expr);                                                  \
+        if (_e != hipSuccess) {                                                  \
+            if (getenv("ZRT_DEBUG"))                                             \
+                fprintf(stderr, "zrt: %s failed: %s (%s:%d)\n", #expr,           \
+                        hipGetErrorString(_e), __FILE__, __LINE__);              \
+            return _e == hipErrorOutOfMemory ? ZRT_ERR_OUT_OF_MEMORY : ZRT_ERR_HIP; \
+        }                                                                        \
+    } while (0)
+
+namespace {
+
+constexpr float kFltEps = 1.1920928955078125e-07f;   // std.math.floatEps(f32)
+constexpr int kBlock = 256;                          // 4 waves
+
+struct TraceParams {
+    float bmin[3], bmax[3];
+    uint32_t res[3];
+    float cs[3];
+    const uint2* cells;
+    const float4* tri_pos;    // 3 per ref: v0, e1, e2 (w unused)
+    const float4* tri_data;   // 4 per ref: n0 n1 n2 uv0 uv1 uv2 mat
+    const DevMat* mats;
+    const float* texels;
+    const double* zig;        // zx[257], zf[257]
+    float org[3], llc[3], right[3], up[3];
+    uint32_t w;
+    const uint32_t* pixlist;
+    uint32_t P;               // pixels of this rank
+    uint32_t s0;              // first sample index of this pass
+    uint32_t total;           // items in this pass
+    uint32_t max_bounce;
+    uint64_t seed;
+    float4* out;              // total
+    uint32_t* counter;
+    unsigned long long* stats;   // segments, cells, tests, hits
+};
+
+// per-bounce (emissive, albedo) pairs in registers; identity = (0, 1) so that
+// pass-through bounces and unused slots fold as e + a*L = L exactly.
+template <int N>
+struct Stack {
+    v3 e[N], a[N];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < N; ++i) { e[i] = mk(0, 0, 0); a[i] = mk(1, 1, 1); }
+    }
+    __device__ __forceinline__ void set(uint32_t slot, v3 ee, v3 aa) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((uint32_t)i == slot) { e[i] = ee; a[i] = aa; }
+    }
+    __device__ __forceinline__ v3 fold(v3 L) const {
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) L = add(e[i], mul(a[i], L));
+        return L;
+    }
+};
+
+// Scene.traceRay (stage3.zig:152-186): nearest hit along the grid DDA.
+template <bool STATS>
+__device__ __forceinline__ float trace_ray(const TraceParams& p, v3 o, v3 d, float& hu, float& hv,
+                                           uint32_t& hidx, uint32_t& n_cells, uint32_t& n_tests) {
+    float nearest = kInf;
+    float t_hit;
+    Bbox bb;
+    bb.min = mk(p.bmin[0], p.bmin[1], p.bmin[2]);
+    bb.max = mk(p.bmax[0], p.bmax[1], p.bmax[2]);
+    if (!bbox_ray(bb, o, d, &t_hit)) return nearest;
+    t_hit = fmaxf(0.0f, t_hit);
+    // Grid.traceRay setup (linalg.zig:450-467), per axis
+    const v3 local = sub(add(o, scale(d, t_hit)), bb.min);
+    const float lq[3] = {local.x, local.y, local.z};
+    const float dq[3] = {d.x, d.y, d.z};
+    uint32_t c[3], ex[3], st[3];
+    float td[3], tn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const bool sg = dq[i] < 0.0f;
+        const uint32_t rm1 = p.res[i] - 1u;
+        uint32_t ci = f2u(lq[i] / p.cs[i]);
+        ci = ci < rm1 ? ci : rm1;
+        c[i] = ci;
+        st[i] = sg ? 0xFFFFFFFFu : 1u;
+        ex[i] = sg ? 0u : rm1;
+        td[i] = fabsf(p.cs[i] / dq[i]);
+        const float next_cell = (float)(ci + (sg ? 0u : 1u));
+        tn[i] = t_hit + ((next_cell * p.cs[i] - lq[i]) / dq[i]);
+    }
+    const uint32_t rx = p.res[0], rxy = p.res[0] * p.res[1];
+    uint32_t lin = c[2] * rxy + c[1] * rx + c[0];
+    const uint32_t dl0 = st[0] == 1u ? 1u : 0xFFFFFFFFu;
+    const uint32_t dl1 = st[1] == 1u ? rx : 0u - rx;
+    const uint32_t dl2 = st[2] == 1u ? rxy : 0u - rxy;
+    for (;;) {
+        const uint2 cell = p.cells[lin];
+        if (STATS) ++n_cells;
+        for (uint32_t i = cell.x; i < cell.y; ++i) {
+            const float4 a = p.tri_pos[3 * i + 0];
+            const float4 b = p.tri_pos[3 * i + 1];
+            const float4 cc = p.tri_pos[3 * i + 2];
+            float t, u, v;
+            if (STATS) ++n_tests;
+            if (tri_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cc.x, cc.y, cc.z), o, d, &t, &u, &v)) {
+                if (nearest > t && t > 0.0f) { nearest = t; hu = u; hv = v; hidx = i; }
+            }
+        }
+        // Iterator.next (linalg.zig:478-496): axis = map[k], map packed 0xA66
+        const unsigned k = ((unsigned)(tn[0] < tn[1]) << 2) | ((unsigned)(tn[0] < tn[2]) << 1) |
+                           (unsigned)(tn[1] < tn[2]);
+        const unsigned axis = (0xA66u >> (2u * k)) & 3u;
+        float t_exit;
+        if (axis == 0) {
+            if (c[0] == ex[0]) t_exit = kInf;
+            else { t_exit = tn[0]; c[0] += st[0]; tn[0] += td[0]; lin += dl0; }
+        } else if (axis == 1) {
+            if (c[1] == ex[1]) t_exit = kInf;
+            else { t_exit = tn[1]; c[1] += st[1]; tn[1] += td[1]; lin += dl1; }
+        } else {
+            if (c[2] == ex[2]) t_exit = kInf;
+            else { t_exit = tn[2]; c[2] += st[2]; tn[2] += td[2]; lin += dl2; }
+        }
+        if (nearest <= t_exit) break;
+    }
+    return nearest;
+}
+
+__device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, float u, float v) {
+    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
+    const float* b = texels + t.off;
+    v3 r;
+    r.x = bilerp(b[3 * c.i11 + 0], b[3 * c.i21 + 0], b[3 * c.i12 + 0], b[3 * c.i22 + 0], c.fu, c.fv);
+    r.y = bilerp(b[3 * c.i11 + 1], b[3 * c.i21 + 1], b[3 * c.i12 + 1], b[3 * c.i22 + 1], c.fu, c.fv);
+    r.z = bilerp(b[3 * c.i11 + 2], b[3 * c.i21 + 2], b[3 * c.i12 + 2], b[3 * c.i22 + 2], c.fu, c.fv);
+    return r;
+}
+__device__ __forceinline__ float sample1(const float* texels, const DevTex& t, float u, float v) {
+    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
+    const float* b = texels + t.off;
+    return bilerp(b[c.i11], b[c.i21], b[c.i12], b[c.i22], c.fu, c.fv);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)x, off);
+        const unsigned hi = __shfl_xor((unsigned)(x >> 32), off);
+        x += ((unsigned long long)hi << 32) | lo;
+    }
+    return x;
+}
+
+template <int MAXB, bool STATS>
+__global__ __launch_bounds__(kBlock) void trace_kernel(const TraceParams p) {
+    __shared__ double s_zig[514];
+    for (int i = threadIdx.x; i < 514; i += kBlock) s_zig[i] = p.zig[i];
+    __syncthreads();
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
+    const v3 org = mk(p.org[0], p.org[1], p.org[2]);
+    const v3 llc = mk(p.llc[0], p.llc[1], p.llc[2]);
+    const v3 right = mk(p.right[0], p.right[1], p.right[2]);
+    const v3 up = mk(p.up[0], p.up[1], p.up[2]);
+
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(p.counter, 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= p.total) break;
+        const uint32_t item = base + lane;
+        if (item >= p.total) continue;
+
+        const uint32_t s_local = item / p.P;
+        const uint32_t q = item - s_local * p.P;
+        const uint32_t sample = p.s0 + s_local;
+        const uint32_t pixel = p.pixlist[q];
+        const uint32_t py = pixel / p.w;
+        const uint32_t px = pixel - py * p.w;
+        Rng rng;
+        rng.s = path_key(p.seed, pixel, sample);
+        // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35)
+        const float jx = rng_float(rng);
+        const float jy = rng_float(rng);
+        v3 o = org;
+        v3 d = normalize(add(add(llc, scale(right, (float)px + jx)), scale(up, (float)py + jy)));
+
+        Stack<MAXB> stk;
+        stk.init();
+        v3 L = mk(0, 0, 0);
+        uint32_t slot = 0;
+        for (uint32_t depth = p.max_bounce; depth > 0; --depth, ++slot) {
+            ++n_seg;
+            float hu = 0.0f, hv = 0.0f;
+            uint32_t hidx = 0;
+            const float t = trace_ray<STATS>(p, o, d, hu, hv, hidx, n_cells, n_tests);
+            if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
+            if (STATS) ++n_hits;
+            // stage3.zig:199-206
+            const float4* td = p.tri_data + 4ull * hidx;
+            const float4 d0 = td[0], d1 = td[1], d2 = td[2], d3 = td[3];
+            const float w0 = 1.0f - hu - hv;
+            const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
+            const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
+            const DevMat& m = p.mats[__float_as_uint(d3.w)];
+            const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
+            const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
+            const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
+            const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
+                               scale(mk(d1.z, d1.w, d2.x), hv));
+            const v3 no = add(o, scale(d, t + kFltEps));        // ray.at(hit.t + eps)
+            if (rng_float(rng) > transparency) {                // stage3.zig:207-213
+                o = no;
+                continue;
+            }
+            // randomUnitVector (linalg.zig:140-148): 3 x floatNorm, normalize
+            const float nx = (float)rng_norm64(rng, zx, zf);
+            const float ny = (float)rng_norm64(rng, zx, zf);
+            const float nz = (float)rng_norm64(rng, zx, zf);
+            d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+            o = no;
+            stk.set(slot, emissive, albedo);                    // stage3.zig:219
+        }
+        L = stk.fold(L);
+        p.out[item] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+    const unsigned long long s0 = wave_sum(n_seg);
+    unsigned long long s1 = 0, s2 = 0, s3 = 0;
+    if (STATS) { s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits); }
+    if (lane == 0) {
+        atomicAdd(&p.stats[0], s0);
+        if (STATS) {
+            atomicAdd(&p.stats[1], s1);
+            atomicAdd(&p.stats[2], s2);
+            atomicAdd(&p.stats[3], s3);
+        }
+    }
+}
+
+// renderWorker tail (stage3.zig:236-242): ordered per-pixel sum over this
+// pass's samples, then (last pass) * (1/spp) and toRGB.
+__global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restrict__ out, uint32_t P,
+                                                         uint32_t S, float4* acc, int first, int last,
+                                                         float inv_spp, uint8_t* rgb, float* lin) {
+    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= P) return;
+    v3 px = mk(0, 0, 0);
+    if (!first) { const float4 a = acc[q]; px = mk(a.x, a.y, a.z); }
+    for (uint32_t s = 0; s < S; ++s) {
+        const float4 c = out[(size_t)s * P + q];
+        px = add(px, mk(c.x, c.y, c.z));
+    }
+    if (!last) { acc[q] = make_float4(px.x, px.y, px.z, 0.0f); return; }
+    const v3 l = mul(px, mk(inv_spp, inv_spp, inv_spp));
+    uint8_t c[3];
+    to_rgb(l, c);
+    rgb[3 * (size_t)q + 0] = c[0];
+    rgb[3 * (size_t)q + 1] = c[1];
+    rgb[3 * (size_t)q + 2] = c[2];
+    if (lin) { lin[3 * (size_t)q] = l.x; lin[3 * (size_t)q + 1] = l.y; lin[3 * (size_t)q + 2] = l.z; }
+}
+
+using TraceFn = void (*)(const TraceParams);
+
+template <int MAXB>
+TraceFn pick(bool stats) {
+    return stats ? (TraceFn)trace_kernel<MAXB, true> : (TraceFn)trace_kernel<MAXB, false>;
+}
+
+TraceFn trace_fn(uint32_t max_bounce, bool stats, int* maxb) {
+    if (max_bounce <= 4) { *maxb = 4; return pick<4>(stats); }
+    if (max_bounce <= 8) { *maxb = 8; return pick<8>(stats); }
+    if (max_bounce <= 16) { *maxb = 16; return pick<16>(stats); }
+    if (max_bounce <= 64) { *maxb = 64; return pick<64>(stats); }
+    return nullptr;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+int grow(T** p, size_t* cap, size_t n) {
+    if (*cap >= n && *p) return ZRT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)));
+    *cap = n;
+    return ZRT_OK;
+}
+
+}  // namespace
+
+struct zrt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    std::vector<hipEvent_t> ev_trace;
+    zrt_grid grid{};
+    uint32_t ncells = 0, nrefs = 0, nmat = 0;
+    uint2* d_cells = nullptr;
+    float4* d_pos = nullptr;
+    float4* d_data = nullptr;
+    DevMat* d_mats = nullptr;
+    float* d_texels = nullptr;
+    double* d_zig = nullptr;
+    // grow-only work buffers
+    uint32_t* d_pix = nullptr; size_t pix_cap = 0;
+    float4* d_out = nullptr; size_t out_cap = 0;
+    float4* d_acc = nullptr; size_t acc_cap = 0;
+    uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
+    float* d_lin = nullptr; size_t lin_cap = 0;
+    uint32_t* d_counter = nullptr;
+    unsigned long long* d_stats = nullptr;
+    int num_cus = 0;
+    // cached pixel list
+    std::vector<uint32_t> pix;
+    uint32_t pix_key[5] = {0, 0, 0, 0, 0};
+    bool pix_valid = false;
+};
+
+static int validate_scene(const zrt_scene* s) {
+    if (!s) return ZRT_ERR_INVALID_ARG;
+    const uint64_t nc = (uint64_t)s->grid.resolution[0] * s->grid.resolution[1] * s->grid.resolution[2];
+    if (nc == 0 || nc != s->num_cells || nc > 0x7FFFFFFFull || !s->cells) return ZRT_ERR_INVALID_ARG;
+    if (s->num_triangles && (!s->triangles_pos || !s->triangles_data || !s->triangles_material))
+        return ZRT_ERR_INVALID_ARG;
+    if (s->num_materials == 0 || !s->materials || !s->texels) return ZRT_ERR_INVALID_ARG;
+    for (uint64_t c = 0; c < nc; ++c) {
+        const uint32_t b = s->cells[2 * c], e = s->cells[2 * c + 1];
+        if (b > e || e > s->num_triangles) return ZRT_ERR_INVALID_ARG;
+    }
+    for (uint32_t i = 0; i < s->num_triangles; ++i)
+        if (s->triangles_material[i] >= s->num_materials) return ZRT_ERR_INVALID_ARG;
+    for (uint32_t m = 0; m < s->num_materials; ++m) {
+        const zrt_texture* t[3] = {&s->materials[m].base_color, &s->materials[m].emissive,
+                                   &s->materials[m].transparency};
+        for (int k = 0; k < 3; ++k) {
+            const uint64_t ch = k < 2 ? 3 : 1;
+            if (t[k]->w <= 0 || t[k]->h <= 0) return ZRT_ERR_INVALID_ARG;
+            if (t[k]->offset + (uint64_t)t[k]->w * t[k]->h * ch > s->num_texel_floats)
+                return ZRT_ERR_INVALID_ARG;
+            if (t[k]->offset > 0xFFFFFFFFull) return ZRT_ERR_UNSUPPORTED;
+        }
+    }
+    return ZRT_OK;
+}
+
+extern "C" int zrt_device_count(int* count) {
+    if (!count) return ZRT_ERR_INVALID_ARG;
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return ZRT_ERR_NO_DEVICE;
+    *count = n;
+    return ZRT_OK;
+}
+
+extern "C" void zrt_context_destroy(zrt_context* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_pix,
+                    c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
+    if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
+    if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int context_init(zrt_context* c, const zrt_scene* s) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&c->ev_begin));
+    HIP_TRY(hipEventCreate(&c->ev_end));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+    c->num_cus = prop.multiProcessorCount;
+    c->grid = s->grid;
+    c->ncells = s->num_cells;
+    c->nrefs = s->num_triangles;
+    c->nmat = s->num_materials;
+    HIP_TRY(hipMalloc((void**)&c->d_cells, 8ull * c->ncells));
+    HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
+    const size_t nr = std::max<size_t>(c->nrefs, 1);
+    std::vector<float4> pos(3 * nr), dat(4 * nr);
+    for (uint32_t i = 0; i < c->nrefs; ++i) {
+        const float* q = s->triangles_pos + 9ull * i;
+        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], 0.0f);
+        pos[3 * i + 1] = make_float4(q[3], q[4], q[5], 0.0f);
+        pos[3 * i + 2] = make_float4(q[6], q[7], q[8], 0.0f);
+        float tmp[16];
+        memcpy(tmp, s->triangles_data + 15ull * i, 15 * sizeof(float));
+        memcpy(&tmp[15], &s->triangles_material[i], 4);
+        memcpy(&dat[4 * i], tmp, 64);
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_pos, pos.size() * sizeof(float4)));
+    HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
+    HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
+    std::vector<DevMat> mats(c->nmat);
+    for (uint32_t m = 0; m < c->nmat; ++m) {
+        const zrt_texture* t[3] = {&s->materials[m].base_color, &s->materials[m].emissive,
+                                   &s->materials[m].transparency};
+        for (int k = 0; k < 3; ++k) {
+            DevTex& d = mats[m].tex[k];
+            d.off = (uint32_t)t[k]->offset;
+            d.w = t[k]->w; d.h = t[k]->h;
+            d.umin = t[k]->u_min; d.umax = t[k]->u_max;
+            d.vmin = t[k]->v_min; d.vmax = t[k]->v_max;
+            d.pad = 0;
+        }
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_mats, mats.size() * sizeof(DevMat)));
+    HIP_TRY(hipMemcpy(c->d_mats, mats.data(), mats.size() * sizeof(DevMat), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&c->d_texels, s->num_texel_floats * sizeof(float)));
+    HIP_TRY(hipMemcpy(c->d_texels, s->texels, s->num_texel_floats * sizeof(float), hipMemcpyHostToDevice));
+    double zig[514];
+    zig_tables(zig, zig + 257);
+    HIP_TRY(hipMalloc((void**)&c->d_zig, sizeof zig));
+    HIP_TRY(hipMemcpy(c->d_zig, zig, sizeof zig, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
+    HIP_TRY(hipMalloc((void**)&c->d_stats, 64));
+    return ZRT_OK;
+}
+
+extern "C" int zrt_context_create(const zrt_scene* s, int device, zrt_context** out) {
+    if (!out) return ZRT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int rc = validate_scene(s);
+    if (rc != ZRT_OK) return rc;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) return ZRT_ERR_NO_DEVICE;
+    }
+    if (device >= n) return ZRT_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    zrt_context* c = new (std::nothrow) zrt_context();
+    if (!c) return ZRT_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    rc = context_init(c, s);
+    if (rc != ZRT_OK) { zrt_context_destroy(c); return rc; }
+    *out = c;
+    return ZRT_OK;
+}
+
+static size_t pass_budget_bytes() {
+    const char* e = getenv("ZRT_PASS_BYTES");
+    if (e) { const long long v = atoll(e); if (v > 0) return (size_t)v; }
+    return (size_t)8 << 30;   // 8 GiB of sample radiance per pass (HBM is 288 GB)
+}
+
+extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const zrt_render_config* cfg,
+                                  const zrt_outputs* outs, zrt_stats* stats) {
+    if (!c || !cam || !cfg) return ZRT_ERR_INVALID_ARG;
+    if (cfg->num_samples == 0 || cfg->num_samples > 65535) return ZRT_ERR_INVALID_ARG;
+    if (cam->w == 0 || cam->h == 0 || (uint64_t)cam->w * cam->h > 0xFFFFFFFFull) return ZRT_ERR_INVALID_ARG;
+    const uint32_t nranks = cfg->num_ranks ? cfg->num_ranks : 1;
+    if (cfg->rank >= nranks) return ZRT_ERR_INVALID_ARG;
+    int maxb = 0;
+    const bool want_stats = (cfg->flags & ZRT_FLAG_COUNT_STATS) != 0;
+    TraceFn fn = trace_fn(cfg->max_bounce, want_stats, &maxb);
+    if (!fn) return ZRT_ERR_UNSUPPORTED;
+    DeviceGuard g(c->device);
+
+    // packed pixel order of this rank (cached across calls)
+    const uint32_t key[5] = {cam->w, cam->h, cfg->tile_size ? cfg->tile_size : 64, cfg->rank, nranks};
+    if (!c->pix_valid || memcmp(key, c->pix_key, sizeof key) != 0) {
+        uint32_t n = 0;
+        int rc = tile_pixels(key[0], key[1], key[2], key[3], key[4], nullptr, &n);
+        if (rc != ZRT_OK) return rc;
+        c->pix.resize(std::max<uint32_t>(n, 1));
+        tile_pixels(key[0], key[1], key[2], key[3], key[4], c->pix.data(), &n);
+        c->pix.resize(n);
+        int r2 = grow(&c->d_pix, &c->pix_cap, std::max<size_t>(n, 1));
+        if (r2 != ZRT_OK) return r2;
+        if (n) HIP_TRY(hipMemcpy(c->d_pix, c->pix.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        memcpy(c->pix_key, key, sizeof key);
+        c->pix_valid = true;
+    }
+    const uint32_t P = (uint32_t)c->pix.size();
+    zrt_stats st{};
+    if (P == 0) { if (stats) *stats = st; return ZRT_OK; }
+
+    const uint32_t spp = cfg->num_samples;
+    uint64_t s_pass = std::max<uint64_t>(1, pass_budget_bytes() / (16ull * P));
+    s_pass = std::min<uint64_t>(s_pass, spp);
+    s_pass = std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
+    const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
+    int rc = grow(&c->d_out, &c->out_cap, (size_t)s_pass * P);
+    if (rc != ZRT_OK) return rc;
+    if (npasses > 1 && (rc = grow(&c->d_acc, &c->acc_cap, P)) != ZRT_OK) return rc;
+    if ((rc = grow(&c->d_rgb, &c->rgb_cap, 3ull * P)) != ZRT_OK) return rc;
+    const bool want_lin = outs && outs->linear_packed;
+    if (want_lin && (rc = grow(&c->d_lin, &c->lin_cap, 3ull * P)) != ZRT_OK) return rc;
+    while (c->ev_trace.size() < 2ull * npasses) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->ev_trace.push_back(e);
+    }
+
+    // occupancy-sized persistent grid
+    int bpc = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)fn, kBlock, 0));
+    bpc = std::max(1, std::min(bpc, 8));
+    const uint32_t grid_blocks = (uint32_t)(c->num_cus * bpc);
+
+    TraceParams tp;
+    memset(&tp, 0, sizeof tp);
+    for (int i = 0; i < 3; ++i) {
+        tp.bmin[i] = c->grid.bbox_min[i];
+        tp.bmax[i] = c->grid.bbox_max[i];
+        tp.res[i] = c->grid.resolution[i];
+        tp.cs[i] = c->grid.cell_size[i];
+        tp.org[i] = cam->origin[i];
+        tp.llc[i] = cam->lower_left_corner[i];
+        tp.right[i] = cam->right[i];
+        tp.up[i] = cam->up[i];
+    }
+    tp.cells = c->d_cells;
+    tp.tri_pos = c->d_pos;
+    tp.tri_data = c->d_data;
+    tp.mats = c->d_mats;
+    tp.texels = c->d_texels;
+    tp.zig = c->d_zig;
+    tp.w = cam->w;
+    tp.pixlist = c->d_pix;
+    tp.P = P;
+    tp.max_bounce = cfg->max_bounce;
+    tp.seed = cfg->seed;
+    tp.out = c->d_out;
+    tp.counter = c->d_counter;
+    tp.stats = c->d_stats;
+    // stage3.zig:223 inv_num_samples = ones / splat(spp)  (f32 division)
+    const float inv_spp = 1.0f / (float)spp;
+
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 64, c->stream));
+    HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
+    for (uint32_t pass = 0; pass < npasses; ++pass) {
+        const uint32_t s0 = (uint32_t)(pass * s_pass);
+        const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
+        tp.s0 = s0;
+        tp.total = S * P;
+        HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
+        HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
+        hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(kBlock), 0, c->stream, tp);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
+        hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                           c->d_out, P, S, c->d_acc, pass == 0 ? 1 : 0, pass + 1 == npasses ? 1 : 0,
+                           inv_spp, c->d_rgb, want_lin ? c->d_lin : nullptr);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev_end, c->stream));
+    if (outs && outs->device_rgb_packed)
+        HIP_TRY(hipMemcpyAsync(outs->device_rgb_packed, c->d_rgb, 3ull * P, hipMemcpyDeviceToDevice,
+                               c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+
+    unsigned long long hs[8];
+    HIP_TRY(hipMemcpy(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
+    st.render_ms = ms;
+    for (uint32_t pass = 0; pass < npasses; ++pass) {
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[2 * pass], c->ev_trace[2 * pass + 1]));
+        st.trace_kernel_ms += t;
+    }
+    st.trace_launches = npasses;
+    st.segments = hs[0];
+    st.cells_visited = hs[1];
+    st.triangle_tests = hs[2];
+    st.hits = hs[3];
+    st.samples = (uint64_t)P * spp;
+
+    if (outs && (outs->rgb_packed || outs->rgb_image)) {
+        std::vector<uint8_t> tmp;
+        uint8_t* dst = outs->rgb_packed;
+        if (!dst) { tmp.resize(3ull * P); dst = tmp.data(); }
+        HIP_TRY(hipMemcpy(dst, c->d_rgb, 3ull * P, hipMemcpyDeviceToHost));
+        if (outs->rgb_image)
+            for (uint32_t q = 0; q < P; ++q) memcpy(outs->rgb_image + 3ull * c->pix[q], dst + 3ull * q, 3);
+    }
+    if (want_lin)
+        HIP_TRY(hipMemcpy(outs->linear_packed, c->d_lin, 3ull * P * sizeof(float), hipMemcpyDeviceToHost));
+    if (stats) *stats = st;
+    return ZRT_OK;
+}
+
+extern "C" int zrt_render(const zrt_scene* scene, const zrt_camera* cam, const zrt_render_config* cfg,
+                          uint8_t* rgb_out, zrt_stats* stats) {
+    if (!scene || !cam || !cfg || !rgb_out) return ZRT_ERR_INVALID_ARG;
+    zrt_context* c = nullptr;
+    int rc = zrt_context_create(scene, cfg->device, &c);
+    if (rc != ZRT_OK) return rc;
+    zrt_render_config one = *cfg;
+    one.rank = 0;
+    one.num_ranks = 1;
+    zrt_outputs o{};
+    o.rgb_image = rgb_out;
+    rc = zrt_context_render(c, cam, &one, &o, stats);
+    zrt_context_destroy(c);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Device-function parity probes: the exact __device__ code paths of the
+// kernel, evaluated on the GPU for the Tier-1 tests.
+namespace {
+
+__global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, const void* aux,
+                             const double* zig) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    switch (which) {
+        case ZRT_PROBE_TRIANGLE: {
+            const float* a = (const float*)in + 15ull * i;
+            float* o = (float*)out + 4ull * i;
+            const v3 v0 = ld3(a), v1 = ld3(a + 3), v2 = ld3(a + 6);
+            float t = 0, u = 0, v = 0;
+            const bool h = tri_ray(v0, sub(v1, v0), sub(v2, v0), ld3(a + 9), ld3(a + 12), &t, &u, &v);
+            o[0] = h ? 1.0f : 0.0f; o[1] = t; o[2] = u; o[3] = v;
+            break;
+        }
+        case ZRT_PROBE_BBOX: {
+            const float* a = (const float*)in + 12ull * i;
+            float* o = (float*)out + 2ull * i;
+            Bbox b; b.min = ld3(a); b.max = ld3(a + 3);
+            float t = 0;
+            const bool h = bbox_ray(b, ld3(a + 6), ld3(a + 9), &t);
+            o[0] = h ? 1.0f : 0.0f; o[1] = h ? t : 0.0f;
+            break;
+        }
+        case ZRT_PROBE_DDA: {
+            // same arithmetic as trace_ray's setup + Iterator.next, recording cells
+            const float* a = (const float*)in + 12ull * i;
+            const uint32_t* res = (const uint32_t*)aux;
+            float* o = (float*)out + (1ull + 4ull * 64) * i;
+            Bbox bb; bb.min = ld3(a); bb.max = ld3(a + 3);
+            const uint32_t r3[3] = {res[0], res[1], res[2]};
+            const Grid g = grid_init(bb, r3);
+            const v3 org = ld3(a + 6), d = ld3(a + 9);
+            float t_hit;
+            if (!bbox_ray(bb, org, d, &t_hit)) { o[0] = -1.0f; break; }
+            t_hit = fmaxf(0.0f, t_hit);
+            const v3 local = sub(add(org, scale(d, t_hit)), bb.min);
+            const float lq[3] = {local.x, local.y, local.z}, dq[3] = {d.x, d.y, d.z};
+            const float csq[3] = {g.cell_size.x, g.cell_size.y, g.cell_size.z};
+            uint32_t c[3], ex[3], st[3];
+            float td[3], tn[3];
+            for (int k = 0; k < 3; ++k) {
+                const bool sg = dq[k] < 0.0f;
+                const uint32_t rm1 = r3[k] - 1u;
+                uint32_t ci = f2u(lq[k] / csq[k]);
+                ci = ci < rm1 ? ci : rm1;
+                c[k] = ci; st[k] = sg ? 0xFFFFFFFFu : 1u; ex[k] = sg ? 0u : rm1;
+                td[k] = fabsf(csq[k] / dq[k]);
+                tn[k] = t_hit + ((((float)(ci + (sg ? 0u : 1u))) * csq[k] - lq[k]) / dq[k]);
+            }
+            int nsteps = 0;
+            while (nsteps < 64) {
+                const unsigned kk = ((unsigned)(tn[0] < tn[1]) << 2) | ((unsigned)(tn[0] < tn[2]) << 1) |
+                                    (unsigned)(tn[1] < tn[2]);
+                const unsigned ax = (0xA66u >> (2u * kk)) & 3u;
+                float te;
+                if (c[ax] == ex[ax]) te = kInf;
+                else { te = tn[ax]; c[ax] += st[ax]; tn[ax] += td[ax]; }
+                float* e = o + 1 + 4 * nsteps;
+                e[0] = (float)c[0]; e[1] = (float)c[1]; e[2] = (float)c[2]; e[3] = te;
+                ++nsteps;
+                if (te == kInf) break;
+            }
+            o[0] = (float)nsteps;
+            break;
+        }
+        case ZRT_PROBE_TO_RGB: {
+            const float* a = (const float*)in + 3ull * i;
+            uint8_t c[3];
+            to_rgb(ld3(a), c);
+            float* o = (float*)out + 3ull * i;
+            o[0] = c[0]; o[1] = c[1]; o[2] = c[2];
+            break;
+        }
+        case ZRT_PROBE_RNG_F32:
+        case ZRT_PROBE_RNG_NORM: {
+            const uint32_t* a = (const uint32_t*)in + 3ull * i;
+            Rng r;
+            r.s = path_key((uint64_t)a[0], a[1], a[2]);
+            float* o = (float*)out + 16ull * i;
+            for (int k = 0; k < 16; ++k)
+                o[k] = which == ZRT_PROBE_RNG_F32 ? rng_float(r) : (float)rng_norm64(r, zig, zig + 257);
+            break;
+        }
+        case ZRT_PROBE_EXP_LOG: {
+            const double x = ((const double*)in)[i];
+            double* o = (double*)out + 2ull * i;
+            o[0] = det_exp(x);
+            o[1] = det_log(x);
+            break;
+        }
+        case ZRT_PROBE_TEXTURE: {
+            // aux: int32 {chans, w, h, umin, umax, vmin, vmax, 0} then texels
+            const int32_t* h = (const int32_t*)aux;
+            DevTex t;
+            t.off = 0; t.w = h[1]; t.h = h[2]; t.umin = h[3]; t.umax = h[4]; t.vmin = h[5]; t.vmax = h[6];
+            const float* tex = (const float*)(h + 8);
+            const float* a = (const float*)in + 2ull * i;
+            float* o = (float*)out + 3ull * i;
+            if (h[0] == 3) {
+                const v3 r = sample3(tex, t, a[0], a[1]);
+                o[0] = r.x; o[1] = r.y; o[2] = r.z;
+            } else {
+                o[0] = sample1(tex, t, a[0], a[1]); o[1] = 0; o[2] = 0;
+            }
+            break;
+        }
+        default:
+            break;
+    }
+}
+
+}  // namespace
+
+extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device) {
+    if (!in || !out || n == 0) return ZRT_ERR_INVALID_ARG;
+    size_t in_sz = 0, out_sz = 0, aux_sz = 0;
+    switch (which) {
+        case ZRT_PROBE_TRIANGLE: in_sz = 60; out_sz = 16; break;
+        case ZRT_PROBE_BBOX: in_sz = 48; out_sz = 8; break;
+        case ZRT_PROBE_DDA: in_sz = 48; out_sz = 4 * (1 + 4 * 64); aux_sz = 12; break;
+        case ZRT_PROBE_TO_RGB: in_sz = 12; out_sz = 12; break;
+        case ZRT_PROBE_RNG_F32:
+        case ZRT_PROBE_RNG_NORM: in_sz = 12; out_sz = 64; break;
+        case ZRT_PROBE_EXP_LOG: in_sz = 8; out_sz = 16; break;
+        case ZRT_PROBE_TEXTURE: {
+            in_sz = 8; out_sz = 12;
+            if (!aux) return ZRT_ERR_INVALID_ARG;
+            const int32_t* h = (const int32_t*)aux;
+            if ((h[0] != 1 && h[0] != 3) || h[1] <= 0 || h[2] <= 0) return ZRT_ERR_INVALID_ARG;
+            aux_sz = 32 + 4ull * h[0] * h[1] * h[2];
+            break;
+        }
+        default: return ZRT_ERR_INVALID_ARG;
+    }
+    if (aux_sz && !aux) return ZRT_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ZRT_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    void *d_in = nullptr, *d_out = nullptr, *d_aux = nullptr;
+    double* d_zig = nullptr;
+    double zig[514];
+    zig_tables(zig, zig + 257);
+    int rc = ZRT_OK;
+    auto cleanup = [&]() {
+        if (d_in) (void)hipFree(d_in);
+        if (d_out) (void)hipFree(d_out);
+        if (d_aux) (void)hipFree(d_aux);
+        if (d_zig) (void)hipFree(d_zig);
+    };
+    auto run = [&]() -> int {
+        HIP_TRY(hipMalloc(&d_in, in_sz * n));
+        HIP_TRY(hipMalloc(&d_out, out_sz * n));
+        HIP_TRY(hipMalloc((void**)&d_zig, sizeof zig));
+        HIP_TRY(hipMemcpy(d_in, in, in_sz * n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_zig, zig, sizeof zig, hipMemcpyHostToDevice));
+        if (aux_sz) {
+            HIP_TRY(hipMalloc(&d_aux, aux_sz));
+            HIP_TRY(hipMemcpy(d_aux, aux, aux_sz, hipMemcpyHostToDevice));
+        }
+        hipLaunchKernelGGL(probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d_in, d_out, n,
+                           d_aux, d_zig);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(out, d_out, out_sz * n, hipMemcpyDeviceToHost));
+        return ZRT_OK;
+    };
+    rc = run();
+    cleanup();
+    return rc;
+}

@@ -1,0 +1,26 @@
+// zrt_internal.h -- types shared by the host code and the CDNA4 kernels.
+#pragma once
+
+#include "../../include/zrt.h"
+#include "zrt_math.h"
+
+namespace zrt {
+
+// Device texture descriptor (stage3.zig:82-92): offset in floats into the
+// texel pool; chans = 3 for colour, 1 for transparency.
+struct DevTex {
+    uint32_t off;
+    int32_t w, h, umin, umax, vmin, vmax;
+    uint32_t pad;
+};
+struct DevMat { DevTex tex[3]; };   // base_color, emissive, transparency
+
+// Ziggurat NormDist tables (Zig std ziggurat.zig ZigTableGen), computed on the
+// host with the deterministic exp/log of zrt_math.h.
+void zig_tables(double zx[257], double zf[257]);
+
+// Host-side packed pixel order of one rank (zrt_tile_pixels).
+int tile_pixels(uint32_t w, uint32_t h, uint32_t tile, uint32_t rank, uint32_t nranks,
+                uint32_t* out, uint32_t* count);
+
+}  // namespace zrt

@@ -1,0 +1,281 @@
+"""ctypes binding of libzrt.so (include/zrt.h) -- the product's C ABI.
+
+No fallback: if the HIP library is missing the import of `lib()` raises, so a
+GPU test can never pass on a silent CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzrt.so")
+_lib = None
+
+ZRT_OK = 0
+STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime error",
+          -4: "out of memory", -5: "unsupported configuration", -6: "I/O error",
+          -7: "parse error", -8: "not found", -9: "camera/output size rules violated"}
+FLAG_COUNT_STATS = 0x1
+
+PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
+PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
+
+
+class ZrtError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__(f"{what}: {STATUS.get(status, status)} ({status})")
+
+
+class Grid(C.Structure):
+    _fields_ = [("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3),
+                ("resolution", C.c_uint32 * 3), ("cell_size", C.c_float * 3)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("w", C.c_int32), ("h", C.c_int32),
+                ("u_min", C.c_int32), ("u_max", C.c_int32), ("v_min", C.c_int32),
+                ("v_max", C.c_int32), ("_pad", C.c_int32)]
+
+
+class Material(C.Structure):
+    _fields_ = [("base_color", Texture), ("emissive", Texture), ("transparency", Texture)]
+
+
+class Scene(C.Structure):
+    _fields_ = [("grid", Grid), ("num_cells", C.c_uint32), ("cells", C.POINTER(C.c_uint32)),
+                ("num_triangles", C.c_uint32), ("triangles_pos", C.POINTER(C.c_float)),
+                ("triangles_data", C.POINTER(C.c_float)),
+                ("triangles_material", C.POINTER(C.c_uint32)), ("num_materials", C.c_uint32),
+                ("materials", C.POINTER(Material)), ("texels", C.POINTER(C.c_float)),
+                ("num_texel_floats", C.c_uint64)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("w", C.c_uint32), ("h", C.c_uint32), ("origin", C.c_float * 3),
+                ("lower_left_corner", C.c_float * 3), ("right", C.c_float * 3),
+                ("up", C.c_float * 3)]
+
+    def as_dict(self):
+        return {"w": self.w, "h": self.h, "origin": list(self.origin),
+                "llc": list(self.lower_left_corner), "right": list(self.right), "up": list(self.up)}
+
+
+class RenderConfig(C.Structure):
+    _fields_ = [("num_samples", C.c_uint32), ("max_bounce", C.c_uint32), ("seed", C.c_uint64),
+                ("device", C.c_int32), ("rank", C.c_uint32), ("num_ranks", C.c_uint32),
+                ("tile_size", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32 * 5)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("segments", C.c_uint64), ("cells_visited", C.c_uint64),
+                ("triangle_tests", C.c_uint64), ("hits", C.c_uint64), ("samples", C.c_uint64),
+                ("render_ms", C.c_double), ("trace_kernel_ms", C.c_double),
+                ("trace_launches", C.c_uint32), ("_pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
+class Outputs(C.Structure):
+    _fields_ = [("rgb_image", C.c_void_p), ("rgb_packed", C.c_void_p),
+                ("linear_packed", C.c_void_p), ("device_rgb_packed", C.c_void_p)]
+
+
+EXPORTS = [
+    "zrt_error_string", "zrt_abi_version", "zrt_device_count", "zrt_geometry_build",
+    "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
+    "zrt_context_create", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
+    "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
+    "zrt_camera_from_matrix", "zrt_probe",
+]
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libzrt.so not built at {LIB_PATH} (run `make` or "
+                          "__graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    L.zrt_error_string.restype = C.c_char_p
+    L.zrt_error_string.argtypes = [C.c_int]
+    L.zrt_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.zrt_geometry_build.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_void_p)]
+    L.zrt_geometry_scene.argtypes = [C.c_void_p, C.POINTER(Scene)]
+    L.zrt_geometry_indices.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint32)),
+                                       C.POINTER(C.c_uint32)]
+    L.zrt_geometry_free.argtypes = [C.c_void_p]
+    L.zrt_geometry_free.restype = None
+    L.zrt_render.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(RenderConfig),
+                             C.c_void_p, C.POINTER(Stats)]
+    L.zrt_context_create.argtypes = [C.POINTER(Scene), C.c_int, C.POINTER(C.c_void_p)]
+    L.zrt_context_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig),
+                                     C.POINTER(Outputs), C.POINTER(Stats)]
+    L.zrt_context_destroy.argtypes = [C.c_void_p]
+    L.zrt_context_destroy.restype = None
+    L.zrt_tile_pixels.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.c_void_p, C.POINTER(C.c_uint32)]
+    L.zrt_camera_from_matrix.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int32,
+                                         C.c_int32, C.POINTER(Camera)]
+    L.zrt_probe.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+    if hasattr(L, "zrt_gltf_load"):
+        L.zrt_gltf_load.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]
+        L.zrt_gltf_soup.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 4 + [
+            C.POINTER(C.c_uint32)]
+        L.zrt_gltf_materials.argtypes = [C.c_void_p, C.POINTER(Scene)]
+        L.zrt_gltf_camera.argtypes = [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32,
+                                      C.POINTER(Camera)]
+        L.zrt_gltf_free.argtypes = [C.c_void_p]
+        L.zrt_gltf_free.restype = None
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != ZRT_OK:
+        raise ZrtError(rc, what)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().zrt_device_count(C.byref(n))
+    return n.value if rc == ZRT_OK else 0
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def camera_from_matrix(m16, yfov, aspect=None, width=None, height=None) -> Camera:
+    """stage1.zig:309-371 loadCamera through the C ABI."""
+    cam = Camera()
+    m = np.ascontiguousarray(m16, np.float32)
+    rc = lib().zrt_camera_from_matrix(m.ctypes.data, float(yfov), 0 if aspect is None else 1,
+                                      0.0 if aspect is None else float(aspect),
+                                      -1 if width is None else int(width),
+                                      -1 if height is None else int(height), C.byref(cam))
+    check(rc, "zrt_camera_from_matrix")
+    return cam
+
+
+def tile_pixels(w, h, tile=64, rank=0, num_ranks=1) -> np.ndarray:
+    n = C.c_uint32(0)
+    check(lib().zrt_tile_pixels(w, h, tile, rank, num_ranks, None, C.byref(n)), "zrt_tile_pixels")
+    out = np.zeros(max(n.value, 1), np.uint32)
+    check(lib().zrt_tile_pixels(w, h, tile, rank, num_ranks, out.ctypes.data, C.byref(n)),
+          "zrt_tile_pixels")
+    return out[:n.value]
+
+
+class Geometry:
+    """stage2.Geometry: build (SAT binning) + bake, on host threads."""
+
+    def __init__(self, pos, nrm, uv, mat, resolution=(128, 128, 128), num_threads=0):
+        self._keep = [np.ascontiguousarray(pos, np.float32), np.ascontiguousarray(nrm, np.float32),
+                      np.ascontiguousarray(uv, np.float32), np.ascontiguousarray(mat, np.uint32)]
+        n = self._keep[3].size
+        res = (C.c_uint32 * 3)(*resolution)
+        h = C.c_void_p()
+        check(lib().zrt_geometry_build(self._keep[0].ctypes.data, self._keep[1].ctypes.data,
+                                       self._keep[2].ctypes.data, self._keep[3].ctypes.data, n,
+                                       res, num_threads, C.byref(h)), "zrt_geometry_build")
+        self._h = h
+        self.scene = Scene()
+        check(lib().zrt_geometry_scene(self._h, C.byref(self.scene)), "zrt_geometry_scene")
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.zrt_geometry_free(self._h)
+            self._h = None
+
+    @property
+    def num_refs(self):
+        return int(self.scene.num_triangles)
+
+    def indices(self):
+        p = C.POINTER(C.c_uint32)()
+        n = C.c_uint32(0)
+        check(lib().zrt_geometry_indices(self._h, C.byref(p), C.byref(n)), "zrt_geometry_indices")
+        return np.ctypeslib.as_array(p, (n.value,)).copy() if n.value else np.zeros(0, np.uint32)
+
+    def cells(self):
+        n = self.scene.num_cells
+        return np.ctypeslib.as_array(self.scene.cells, (n, 2)).copy()
+
+    def tri_pos(self):
+        return np.ctypeslib.as_array(self.scene.triangles_pos, (self.num_refs, 9)).copy()
+
+
+def attach_materials(scene: Scene, tex_desc: np.ndarray, texels: np.ndarray, keep: list):
+    """Fill the material fields of a zrt_scene from (nmat,3,7) descriptors."""
+    td = np.asarray(tex_desc, np.int64).reshape(-1, 3, 7)
+    mats = (Material * len(td))()
+    for i, m in enumerate(td):
+        for k, name in enumerate(("base_color", "emissive", "transparency")):
+            t = getattr(mats[i], name)
+            t.offset, t.w, t.h, t.u_min, t.u_max, t.v_min, t.v_max = (int(x) for x in m[k])
+    tx = np.ascontiguousarray(texels, np.float32)
+    keep += [mats, tx]
+    scene.num_materials = len(td)
+    scene.materials = C.cast(mats, C.POINTER(Material))
+    scene.texels = _ptr(tx, C.c_float)
+    scene.num_texel_floats = tx.size
+
+
+class Context:
+    """Device-resident scene (zrt_context): upload once, render many times."""
+
+    def __init__(self, scene: Scene, device: int = -1):
+        h = C.c_void_p()
+        check(lib().zrt_context_create(C.byref(scene), device, C.byref(h)), "zrt_context_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.zrt_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def render(self, cam: Camera, spp: int, max_bounce: int, seed: int = 0, rank: int = 0,
+               num_ranks: int = 1, tile: int = 64, stats: bool = False, image=None,
+               packed=False, linear=False, device_ptr=None):
+        cfg = RenderConfig()
+        cfg.num_samples, cfg.max_bounce, cfg.seed = spp, max_bounce, seed
+        cfg.device, cfg.rank, cfg.num_ranks, cfg.tile_size = -1, rank, num_ranks, tile
+        cfg.flags = FLAG_COUNT_STATS if stats else 0
+        n = None
+        out = Outputs()
+        res = {}
+        if image is not None:
+            out.rgb_image = image.ctypes.data
+        if packed or linear:
+            n = int(tile_pixels(cam.w, cam.h, tile, rank, num_ranks).size)
+        if packed:
+            res["packed"] = np.zeros((n, 3), np.uint8)
+            out.rgb_packed = res["packed"].ctypes.data
+        if linear:
+            res["linear"] = np.zeros((n, 3), np.float32)
+            out.linear_packed = res["linear"].ctypes.data
+        if device_ptr is not None:
+            out.device_rgb_packed = device_ptr
+        st = Stats()
+        check(lib().zrt_context_render(self._h, C.byref(cam), C.byref(cfg), C.byref(out),
+                                       C.byref(st)), "zrt_context_render")
+        res["stats"] = st.as_dict()
+        return res
+
+
+def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=None, device=-1):
+    inp = np.ascontiguousarray(inp)
+    out = np.zeros(out_shape, out_dtype)
+    auxp = None if aux is None else np.ascontiguousarray(aux).ctypes.data
+    check(lib().zrt_probe(which, inp.ctypes.data, out.ctypes.data, n, auxp, device), "zrt_probe")
+    return out

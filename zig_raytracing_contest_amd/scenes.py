@@ -1,0 +1,525 @@
+"""Synthetic scenes for the BASELINE.json configs (the real assets are absent).
+
+The reference renders glTF triangle meshes only (stage1.zig:217-259) and ships
+no scenes; the contest `round1.gltf`, Sponza and the Khronos test scenes are in
+an external repo that is not in this container.  Every config
+is therefore a deterministic procedural stand-in, generated here:
+
+  cfg1  sphere   UV sphere 64x32 (3,968 tris), 256x256, 1 spp
+  cfg2  cornell  Cornell box + emissive ceiling quad, 512x512, 64 spp
+  cfg3  contest  ~100k-tri field ("Camera 1", aspect 16:9, --height 1080), 256 spp
+  cfg4  contest  same scene, 3840x2160, 1024 spp (8 GPUs)
+  cfg5  sponza   ~260k-tri colonnade interior, 1920x1080, 512 spp
+
+A scene is a `SceneSoup`: the flat triangle soup exactly as stage1.loadGeometry
+would produce it (world-space positions, transformDirection+normalize'd
+normals, raw texcoords, material index per triangle), the material/texture
+table exactly as stage1.loadMaterials would (linear float texels, factor
+multiplied, 1x1 dummies), and the glTF camera (node matrix, yfov, aspect).
+`write_gltf` emits the same scene as .gltf + .bin + .png so the C++ loader and
+CLI see identical data.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+F32 = np.float32
+INT_MIN = -2147483648
+INT_MAX = 2147483647
+
+
+# ----------------------------------------------------------------- f32 helpers
+def f32_normalize(v: np.ndarray) -> np.ndarray:
+    """linalg.zig:123 normalize in exact f32: v * (1 / sqrt((x*x + y*y) + z*z))."""
+    v = np.asarray(v, F32)
+    x, y, z = v[..., 0], v[..., 1], v[..., 2]
+    ln = np.sqrt((x * x + y * y) + z * z).astype(F32)
+    inv = (F32(1.0) / ln).astype(F32)
+    return (v * inv[..., None]).astype(F32)
+
+
+def srgb8_to_linear(c: np.ndarray) -> np.ndarray:
+    """stb_image stbi__ldr_to_hdr: (float)pow(x/255.0f, 2.2f) (double pow)."""
+    x = (np.asarray(c, np.uint8).astype(F32) / F32(255.0)).astype(np.float64)
+    return np.power(x, np.float64(F32(2.2))).astype(F32)
+
+
+def alpha8_to_float(a: np.ndarray) -> np.ndarray:
+    return (np.asarray(a, np.uint8).astype(F32) / F32(255.0)).astype(F32)
+
+
+# ------------------------------------------------------------------ materials
+@dataclasses.dataclass
+class Texture:
+    """An 8-bit RGBA image as decoded by stb (rows top->bottom)."""
+    rgba: np.ndarray                 # (h, w, 4) uint8
+    wrap_s_clamp: bool = False       # glTF sampler wrapS == CLAMP_TO_EDGE
+    wrap_t_clamp: bool = False
+    has_alpha: bool = True           # image.actual_c == 4
+
+
+@dataclasses.dataclass
+class Material:
+    base_color: Tuple[float, float, float, float] = (1.0, 1.0, 1.0, 1.0)
+    base_texture: Optional[int] = None
+    emissive: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    emissive_texture: Optional[int] = None
+    alpha_mode: str = "OPAQUE"       # OPAQUE | MASK | BLEND
+    alpha_cutoff: float = 0.5
+    name: str = ""
+
+
+@dataclasses.dataclass
+class CameraDef:
+    name: str
+    matrix: np.ndarray               # column-major 4x4 global transform (16 f32)
+    yfov: float
+    aspect: Optional[float]
+
+
+@dataclasses.dataclass
+class SceneSoup:
+    name: str
+    pos: np.ndarray                  # (n, 9) f32 v0 v1 v2
+    nrm: np.ndarray                  # (n, 9) f32
+    uv: np.ndarray                   # (n, 6) f32
+    mat: np.ndarray                  # (n,) u32
+    materials: List[Material]
+    textures: List[Texture]
+    cameras: List[CameraDef]
+    tex_desc: np.ndarray = None      # (nmat, 3, 7) i32 {off,w,h,umin,umax,vmin,vmax}
+    texels: np.ndarray = None        # f32 pool
+
+    @property
+    def num_triangles(self) -> int:
+        return int(self.pos.shape[0])
+
+    @property
+    def num_materials(self) -> int:
+        return len(self.materials)
+
+    def bake_materials(self):
+        """stage1.zig:381-496 loadMaterials, restated on numpy."""
+        pool: List[np.ndarray] = []
+        size = 0
+        desc = np.zeros((len(self.materials), 3, 7), np.int32)
+
+        def push(arr):
+            nonlocal size
+            off = size
+            a = np.ascontiguousarray(arr, F32).reshape(-1)
+            pool.append(a)
+            size += a.size
+            return off
+
+        def tex_params(t: Texture):
+            h, w = t.rgba.shape[:2]
+            umin, umax = (0, w - 1) if t.wrap_s_clamp else (INT_MIN, INT_MAX)
+            vmin, vmax = (0, h - 1) if t.wrap_t_clamp else (INT_MIN, INT_MAX)
+            return w, h, umin, umax, vmin, vmax
+
+        for m_i, m in enumerate(self.materials):
+            # base colour (loadColorTexture): texel.rgb * factor.rgb, else dummy factor
+            for slot, (tex_i, factor) in enumerate(((m.base_texture, m.base_color[:3]),
+                                                    (m.emissive_texture, m.emissive))):
+                f = np.asarray(factor, F32)
+                if tex_i is None:
+                    off = push(f)
+                    desc[m_i, slot] = (off, 1, 1, 0, 0, 0, 0)
+                else:
+                    t = self.textures[tex_i]
+                    lin = srgb8_to_linear(t.rgba[..., :3]).reshape(-1, 3)
+                    off = push((lin * f).astype(F32))
+                    desc[m_i, slot] = (off,) + tex_params(t)
+            # transparency (loadTransparencyTexture)
+            done = False
+            if m.alpha_mode != "OPAQUE" and m.base_texture is not None:
+                t = self.textures[m.base_texture]
+                if t.has_alpha:
+                    a = alpha8_to_float(t.rgba[..., 3]).reshape(-1)
+                    if m.alpha_mode == "MASK":
+                        a = np.where(a > F32(m.alpha_cutoff), F32(1.0), F32(0.0)).astype(F32)
+                    off = push(a)
+                    desc[m_i, 2] = (off,) + tex_params(t)
+                    done = True
+            if not done:
+                off = push(np.asarray([1.0], F32))
+                desc[m_i, 2] = (off, 1, 1, 0, 0, 0, 0)
+        self.tex_desc = desc
+        self.texels = np.concatenate(pool).astype(F32) if pool else np.zeros(1, F32)
+        return self
+
+    def camera(self, name: Optional[str] = None) -> CameraDef:
+        """stage1.zig:282-296 findCameraIndex."""
+        if not self.cameras:
+            raise ValueError("NoCamerasAtAll")
+        if name is None:
+            return self.cameras[0]
+        for c in self.cameras:
+            if c.name == name:
+                return c
+        raise ValueError("CameraNotFound")
+
+
+# ------------------------------------------------------------ mesh builder
+class MeshBuilder:
+    def __init__(self):
+        self.pos: List[np.ndarray] = []
+        self.nrm: List[np.ndarray] = []
+        self.uv: List[np.ndarray] = []
+        self.mat: List[np.ndarray] = []
+
+    def add(self, verts, normals, uvs, tris, mat):
+        verts = np.asarray(verts, F32)
+        normals = f32_normalize(np.asarray(normals, F32))
+        uvs = np.asarray(uvs, F32)
+        tris = np.asarray(tris, np.int64).reshape(-1, 3)
+        self.pos.append(verts[tris].reshape(-1, 9))
+        self.nrm.append(normals[tris].reshape(-1, 9))
+        self.uv.append(uvs[tris].reshape(-1, 6))
+        self.mat.append(np.full(tris.shape[0], mat, np.uint32))
+
+    def quad(self, p0, p1, p2, p3, mat, uv_scale=(1.0, 1.0), nu=1, nv=1):
+        """Planar quad p0->p1->p2->p3 (CCW seen from the front), nu x nv cells."""
+        p0, p1, p2, p3 = (np.asarray(p, np.float64) for p in (p0, p1, p2, p3))
+        n = np.cross(p1 - p0, p3 - p0)
+        n /= np.linalg.norm(n)
+        s = np.linspace(0, 1, nu + 1)
+        t = np.linspace(0, 1, nv + 1)
+        S, T = np.meshgrid(s, t, indexing="xy")
+        P = ((1 - S)[..., None] * (1 - T)[..., None] * p0 + S[..., None] * (1 - T)[..., None] * p1 +
+             S[..., None] * T[..., None] * p2 + (1 - S)[..., None] * T[..., None] * p3)
+        verts = P.reshape(-1, 3)
+        uvs = np.stack([S.reshape(-1) * uv_scale[0], T.reshape(-1) * uv_scale[1]], -1)
+        idx = np.arange((nu + 1) * (nv + 1)).reshape(nv + 1, nu + 1)
+        a, b = idx[:-1, :-1], idx[:-1, 1:]
+        c, d = idx[1:, 1:], idx[1:, :-1]
+        tris = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3),
+                               np.stack([a, c, d], -1).reshape(-1, 3)])
+        self.add(verts, np.repeat(n[None], len(verts), 0), uvs, tris, mat)
+
+    def box(self, lo, hi, mat, inward=False, n_sub=1):
+        lo, hi = np.asarray(lo, np.float64), np.asarray(hi, np.float64)
+        x0, y0, z0 = lo
+        x1, y1, z1 = hi
+        faces = [  # outward CCW
+            ((x0, y0, z1), (x1, y0, z1), (x1, y1, z1), (x0, y1, z1)),  # +z
+            ((x1, y0, z0), (x0, y0, z0), (x0, y1, z0), (x1, y1, z0)),  # -z
+            ((x1, y0, z1), (x1, y0, z0), (x1, y1, z0), (x1, y1, z1)),  # +x
+            ((x0, y0, z0), (x0, y0, z1), (x0, y1, z1), (x0, y1, z0)),  # -x
+            ((x0, y1, z1), (x1, y1, z1), (x1, y1, z0), (x0, y1, z0)),  # +y
+            ((x0, y0, z0), (x1, y0, z0), (x1, y0, z1), (x0, y0, z1)),  # -y
+        ]
+        for f in faces:
+            if inward:
+                f = (f[0], f[3], f[2], f[1])
+            self.quad(*f, mat=mat, nu=n_sub, nv=n_sub)
+
+    def sphere(self, center, radius, mat, seg_u=64, seg_v=32):
+        """UV sphere: seg_u*2 pole triangles + seg_u*(seg_v-2)*2 = 3,968 at 64x32."""
+        c = np.asarray(center, np.float64)
+        verts, normals, uvs = [], [], []
+        for j in range(seg_v + 1):
+            th = math.pi * j / seg_v
+            for i in range(seg_u + 1):
+                ph = 2 * math.pi * i / seg_u
+                n = np.array([math.sin(th) * math.cos(ph), math.cos(th), -math.sin(th) * math.sin(ph)])
+                verts.append(c + radius * n)
+                normals.append(n)
+                uvs.append((i / seg_u, j / seg_v))
+        tris = []
+        W = seg_u + 1
+        for j in range(seg_v):
+            for i in range(seg_u):
+                a, b = j * W + i, j * W + i + 1
+                cc, d = (j + 1) * W + i + 1, (j + 1) * W + i
+                if j != 0:
+                    tris.append((a, d, b))
+                if j != seg_v - 1:
+                    tris.append((b, d, cc))
+        self.add(np.array(verts), np.array(normals), np.array(uvs), np.array(tris), mat)
+
+    def cylinder(self, base, radius, height, mat, seg=32, rings=8, caps=True):
+        b = np.asarray(base, np.float64)
+        verts, normals, uvs, tris = [], [], [], []
+        W = seg + 1
+        for j in range(rings + 1):
+            y = height * j / rings
+            for i in range(seg + 1):
+                ph = 2 * math.pi * i / seg
+                n = np.array([math.cos(ph), 0.0, -math.sin(ph)])
+                verts.append(b + np.array([radius * n[0], y, radius * n[2]]))
+                normals.append(n)
+                uvs.append((i / seg, j / rings))
+        for j in range(rings):
+            for i in range(seg):
+                a, bb = j * W + i, j * W + i + 1
+                c, d = (j + 1) * W + i + 1, (j + 1) * W + i
+                tris += [(a, bb, c), (a, c, d)]
+        self.add(np.array(verts), np.array(normals), np.array(uvs), np.array(tris), mat)
+        if caps:
+            for top in (False, True):
+                y = height if top else 0.0
+                cv = [b + np.array([0, y, 0])]
+                for i in range(seg):
+                    ph = 2 * math.pi * i / seg
+                    cv.append(b + np.array([radius * math.cos(ph), y, -radius * math.sin(ph)]))
+                nn = np.array([0, 1.0 if top else -1.0, 0])
+                ct = []
+                for i in range(seg):
+                    i0, i1 = 1 + i, 1 + (i + 1) % seg
+                    ct.append((0, i0, i1) if top else (0, i1, i0))
+                self.add(np.array(cv), np.repeat(nn[None], len(cv), 0),
+                         np.zeros((len(cv), 2)), np.array(ct), mat)
+
+    def torus(self, center, R, r, mat, seg_u=24, seg_v=12, axis_up=True):
+        c = np.asarray(center, np.float64)
+        verts, normals, uvs, tris = [], [], [], []
+        W = seg_v + 1
+        for i in range(seg_u + 1):
+            u = 2 * math.pi * i / seg_u
+            for j in range(seg_v + 1):
+                v = 2 * math.pi * j / seg_v
+                n = np.array([math.cos(v) * math.cos(u), math.sin(v), -math.cos(v) * math.sin(u)])
+                p = np.array([(R + r * math.cos(v)) * math.cos(u), r * math.sin(v),
+                              -(R + r * math.cos(v)) * math.sin(u)])
+                if not axis_up:  # rotate so the ring stands upright (xy plane)
+                    n = np.array([n[0], -n[2], n[1]])
+                    p = np.array([p[0], -p[2], p[1]])
+                verts.append(c + p)
+                normals.append(n)
+                uvs.append((i / seg_u, j / seg_v))
+        for i in range(seg_u):
+            for j in range(seg_v):
+                a, b = i * W + j, (i + 1) * W + j
+                cc, d = (i + 1) * W + j + 1, i * W + j + 1
+                tris += [(a, b, cc), (a, cc, d)]
+        self.add(np.array(verts), np.array(normals), np.array(uvs), np.array(tris), mat)
+
+    def soup(self):
+        return (np.concatenate(self.pos), np.concatenate(self.nrm), np.concatenate(self.uv),
+                np.concatenate(self.mat))
+
+
+def look_at(eye, target, up=(0.0, 1.0, 0.0)) -> np.ndarray:
+    """Column-major camera node matrix (camera looks down its local -z)."""
+    eye, target, up = (np.asarray(v, np.float64) for v in (eye, target, up))
+    f = target - eye
+    f /= np.linalg.norm(f)
+    z = -f
+    x = np.cross(up, z)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    m = np.eye(4)
+    m[:3, 0], m[:3, 1], m[:3, 2], m[:3, 3] = x, y, z, eye
+    return m.T.reshape(-1).astype(F32)  # column-major flat
+
+
+def _checker(n=64, cells=8, c0=(230, 230, 230), c1=(40, 40, 40), alpha=255):
+    img = np.zeros((n, n, 4), np.uint8)
+    yy, xx = np.mgrid[0:n, 0:n]
+    m = ((yy * cells // n) + (xx * cells // n)) % 2 == 0
+    img[..., :3] = np.where(m[..., None], np.array(c0, np.uint8), np.array(c1, np.uint8))
+    img[..., 3] = alpha
+    return img
+
+
+def _leaf_mask(n=32, seed=0):
+    rng = np.random.default_rng(seed)
+    img = np.zeros((n, n, 4), np.uint8)
+    yy, xx = np.mgrid[0:n, 0:n] / (n - 1) * 2 - 1
+    r = xx * xx / 0.5 + yy * yy
+    img[..., 0] = 60 + rng.integers(0, 40, (n, n))
+    img[..., 1] = 150 + rng.integers(0, 60, (n, n))
+    img[..., 2] = 50
+    img[..., 3] = np.where(r < 0.9, 255, 0).astype(np.uint8)
+    return img
+
+
+# --------------------------------------------------------------------- scenes
+def sphere_scene() -> SceneSoup:
+    mb = MeshBuilder()
+    mb.sphere((0, 0, 0), 1.0, mat=0, seg_u=64, seg_v=32)
+    pos, nrm, uv, mat = mb.soup()
+    cam = CameraDef("Camera", look_at((0, 0, 3), (0, 0, 0)), math.radians(45.0), None)
+    return SceneSoup("sphere", pos, nrm, uv, mat, [Material(base_color=(0.8, 0.8, 0.8, 1.0))],
+                     [], [cam]).bake_materials()
+
+
+def cornell_scene() -> SceneSoup:
+    """Cornell box.  Side s = 5.0 (exact in f32) on purpose: with s = 5.55 the
+    walls lying on the grid-bbox planes are dropped by the reference's own SAT
+    test (center/extents rounding, linalg.zig:516-522) -- a faithful quirk that
+    tests/test_parity_build.py::test_boundary_wall_quirk pins instead."""
+    mb = MeshBuilder()
+    W, R, G, L = 0, 1, 2, 3
+    s = 5.0
+    # walls, wound so the front faces look into the box (back-face culling)
+    mb.quad((0, 0, 0), (s, 0, 0), (s, 0, -s), (0, 0, -s), W)           # floor (up)
+    mb.quad((0, s, -s), (s, s, -s), (s, s, 0), (0, s, 0), W)           # ceiling (down)
+    mb.quad((0, 0, -s), (s, 0, -s), (s, s, -s), (0, s, -s), W)         # back (+z)
+    mb.quad((0, 0, 0), (0, 0, -s), (0, s, -s), (0, s, 0), R)           # left (+x)
+    mb.quad((s, 0, -s), (s, 0, 0), (s, s, 0), (s, s, -s), G)           # right (-x)
+    # light quad just under the ceiling, facing down
+    mb.quad((2.0, 4.99, -2.0), (3.0, 4.99, -2.0), (3.0, 4.99, -3.0), (2.0, 4.99, -3.0), L)
+    mb.box((1.2, 0.0, -2.2), (2.7, 1.5, -0.7), W)                      # short block
+    mb.box((2.4, 0.0, -4.2), (3.9, 3.0, -2.7), W)                      # tall block
+    pos, nrm, uv, mat = mb.soup()
+    mats = [Material(base_color=(0.73, 0.73, 0.73, 1)), Material(base_color=(0.65, 0.05, 0.05, 1)),
+            Material(base_color=(0.12, 0.45, 0.15, 1)),
+            Material(base_color=(0.78, 0.78, 0.78, 1), emissive=(15.0, 15.0, 15.0))]
+    cam = CameraDef("Camera", look_at((2.5, 2.5, 7.2), (2.5, 2.5, -2.5)), math.radians(39.0), None)
+    return SceneSoup("cornell", pos, nrm, uv, mat, mats, [], [cam]).bake_materials()
+
+
+def cornell_555_scene() -> SceneSoup:
+    """The s = 5.55 box whose bbox-plane walls the reference's SAT drops."""
+    sc = cornell_scene()
+    k = np.float32(5.55 / 5.0)
+    pos = (sc.pos.astype(np.float64) * float(k)).astype(F32)
+    sc.pos = pos
+    sc.name = "cornell555"
+    return sc
+
+
+def contest_scene(seed: int = 12345) -> SceneSoup:
+    """~100k-triangle stand-in for the contest Round1 scene ("Camera 1")."""
+    rng = np.random.default_rng(seed)
+    mb = MeshBuilder()
+    textures = [Texture(_checker(64, 8)), Texture(_leaf_mask(32, seed), wrap_s_clamp=True,
+                                                  wrap_t_clamp=True)]
+    mats = [
+        Material(base_color=(0.9, 0.9, 0.9, 1), base_texture=0, name="ground"),   # 0 textured
+        Material(base_color=(0.8, 0.3, 0.2, 1), name="red"),                      # 1
+        Material(base_color=(0.2, 0.5, 0.8, 1), name="blue"),                     # 2
+        Material(base_color=(0.85, 0.85, 0.5, 1), name="yellow"),                 # 3
+        Material(base_color=(0.9, 0.9, 0.9, 1), emissive=(4.0, 3.5, 2.5), name="lamp"),  # 4
+        Material(base_color=(1, 1, 1, 1), base_texture=1, alpha_mode="MASK",
+                 alpha_cutoff=0.5, name="leaf"),                                  # 5
+        Material(base_color=(0.6, 0.6, 0.6, 1), name="grey"),                     # 6
+    ]
+    mb.quad((-40, 0, 40), (40, 0, 40), (40, 0, -40), (-40, 0, -40), 0, uv_scale=(20, 20),
+            nu=100, nv=100)
+    for _ in range(70):
+        r = float(rng.uniform(0.5, 2.0))
+        x, z = rng.uniform(-30, 30, 2)
+        mb.sphere((x, r, z), r, int(rng.choice([1, 2, 3, 6])), seg_u=32, seg_v=16)
+    for _ in range(6):
+        r = float(rng.uniform(0.4, 0.8))
+        x, z = rng.uniform(-25, 25, 2)
+        mb.sphere((x, r + 3.0, z), r, 4, seg_u=32, seg_v=16)
+    for _ in range(30):
+        x, z = rng.uniform(-30, 30, 2)
+        h = float(rng.uniform(1, 6))
+        w = float(rng.uniform(0.5, 2))
+        mb.box((x - w, 0, z - w), (x + w, h, z + w), int(rng.choice([1, 2, 3, 6])))
+    for _ in range(10):
+        x, z = rng.uniform(-25, 25, 2)
+        mb.torus((x, 2.0, z), 1.5, 0.4, int(rng.choice([1, 2, 3])), axis_up=bool(rng.integers(2)))
+    for _ in range(200):   # alpha-masked leaf cards
+        x, z = rng.uniform(-30, 30, 2)
+        y = float(rng.uniform(0.5, 6))
+        a = float(rng.uniform(0, 2 * math.pi))
+        dx, dz = math.cos(a) * 0.7, math.sin(a) * 0.7
+        mb.quad((x - dx, y - 0.7, z - dz), (x + dx, y - 0.7, z + dz), (x + dx, y + 0.7, z + dz),
+                (x - dx, y + 0.7, z - dz), 5)
+    pos, nrm, uv, mat = mb.soup()
+    cams = [CameraDef("Camera 1", look_at((0, 9, 42), (0, 1, 0)), math.radians(50.0), 16 / 9),
+            CameraDef("Camera 2", look_at((30, 20, 30), (0, 0, 0)), math.radians(45.0), 16 / 9)]
+    return SceneSoup("contest", pos, nrm, uv, mat, mats, textures, cams).bake_materials()
+
+
+def sponza_scene(seed: int = 12345) -> SceneSoup:
+    """~260k-triangle colonnade interior: dense cells, long corridors."""
+    rng = np.random.default_rng(seed)
+    mb = MeshBuilder()
+    textures = [Texture(_checker(128, 16, (200, 180, 150), (120, 100, 80)))]
+    mats = [Material(base_color=(0.9, 0.9, 0.9, 1), base_texture=0, name="floor"),
+            Material(base_color=(0.75, 0.7, 0.6, 1), name="stone"),
+            Material(base_color=(0.7, 0.1, 0.1, 1), name="cloth_red"),
+            Material(base_color=(0.1, 0.2, 0.6, 1), name="cloth_blue"),
+            Material(base_color=(0.8, 0.8, 0.8, 1), emissive=(6.0, 5.0, 3.0), name="lamp")]
+    L, Wd, H = 30.0, 12.0, 12.0
+    mb.quad((-L, 0, Wd), (L, 0, Wd), (L, 0, -Wd), (-L, 0, -Wd), 0, uv_scale=(30, 12), nu=150, nv=60)
+    # side walls facing inward
+    mb.quad((-L, 0, -Wd), (L, 0, -Wd), (L, H, -Wd), (-L, H, -Wd), 1, nu=120, nv=24)
+    mb.quad((L, 0, Wd), (-L, 0, Wd), (-L, H, Wd), (L, H, Wd), 1, nu=120, nv=24)
+    # end walls
+    mb.quad((-L, 0, Wd), (-L, 0, -Wd), (-L, H, -Wd), (-L, H, Wd), 1, nu=48, nv=24)
+    mb.quad((L, 0, -Wd), (L, 0, Wd), (L, H, Wd), (L, H, -Wd), 1, nu=48, nv=24)
+    # roof strips (the centre stays open to the sky)
+    for zs in ((-Wd, -4.0), (4.0, Wd)):
+        mb.quad((-L, H, zs[1]), (L, H, zs[1]), (L, H, zs[0]), (-L, H, zs[0]), 1, nu=60, nv=8)
+    # two colonnades, two levels
+    for z in (-6.0, 6.0):
+        for k in range(13):
+            x = -27 + k * 4.5
+            mb.cylinder((x, 0, z), 0.45, 5.5, 1, seg=48, rings=40)
+            mb.cylinder((x, 6.0, z), 0.3, 5.0, 1, seg=32, rings=20)
+            mb.box((x - 0.7, 5.5, z - 0.7), (x + 0.7, 6.0, z + 0.7), 1, n_sub=4)
+            if k < 12:
+                mb.torus((x + 2.25, 5.5, z), 2.25, 0.3, 1, seg_u=48, seg_v=12, axis_up=False)
+        # gallery floor
+        zz = (z - 1.2, z + 1.2) if z < 0 else (z - 1.2, z + 1.2)
+        mb.quad((-L, 6.0, zz[1]), (L, 6.0, zz[1]), (L, 6.0, zz[0]), (-L, 6.0, zz[0]), 1, nu=60, nv=4)
+    # draperies: wavy cloth panels
+    for k in range(10):
+        x0 = -25 + k * 5.0
+        z = -9.0 if k % 2 == 0 else 9.0
+        n = 40
+        verts, normals, uvs = [], [], []
+        for j in range(n + 1):
+            for i in range(n + 1):
+                s, t = i / n, j / n
+                off = 0.3 * math.sin(s * 6 * math.pi) * (1 - t)
+                zz = z + (off if z < 0 else -off)
+                verts.append((x0 + 3.0 * s, 10.5 - 6.0 * t, zz))
+                dz = 0.3 * 6 * math.pi * math.cos(s * 6 * math.pi) * (1 - t) / 3.0
+                nz = 1.0 if z < 0 else -1.0
+                normals.append((-dz * nz, 0.0, nz))
+                uvs.append((s, t))
+        tris = []
+        for j in range(n):
+            for i in range(n):
+                a, b = j * (n + 1) + i, j * (n + 1) + i + 1
+                c, d = (j + 1) * (n + 1) + i + 1, (j + 1) * (n + 1) + i
+                tris += [(a, d, c), (a, c, b)] if z < 0 else [(a, b, c), (a, c, d)]
+        mb.add(np.array(verts), np.array(normals), np.array(uvs), np.array(tris), 2 + (k % 2))
+    # clutter: urns and lamps along the hall
+    for _ in range(24):
+        x = float(rng.uniform(-26, 26))
+        z = float(rng.choice([-3.0, 3.0]))
+        mb.sphere((x, 0.6, z), 0.6, 1, seg_u=32, seg_v=16)
+    for k in range(8):
+        mb.sphere((-24 + k * 7.0, 9.5, 0.0), 0.35, 4, seg_u=24, seg_v=12)
+    pos, nrm, uv, mat = mb.soup()
+    cams = [CameraDef("Camera", look_at((-26.0, 2.5, 0.5), (10.0, 4.0, 0.0)), math.radians(60.0),
+                      16 / 9)]
+    return SceneSoup("sponza", pos, nrm, uv, mat, mats, textures, cams).bake_materials()
+
+
+SCENES = {"sphere": sphere_scene, "cornell": cornell_scene, "contest": contest_scene,
+          "sponza": sponza_scene, "cornell555": cornell_555_scene}
+
+# BASELINE.json configs -> (scene, camera name, width, height, spp, max_bounce)
+CONFIGS = {
+    "cfg1": dict(scene="sphere", camera=None, width=256, height=256, spp=1, max_bounce=4),
+    "cfg2": dict(scene="cornell", camera=None, width=512, height=512, spp=64, max_bounce=4),
+    "cfg3": dict(scene="contest", camera="Camera 1", width=None, height=1080, spp=256,
+                 max_bounce=4),
+    "cfg4": dict(scene="contest", camera="Camera 1", width=None, height=2160, spp=1024,
+                 max_bounce=4),
+    "cfg5": dict(scene="sponza", camera=None, width=None, height=1080, spp=512, max_bounce=4),
+}
+
+_cache = {}
+
+
+def get_scene(name: str) -> SceneSoup:
+    if name not in _cache:
+        _cache[name] = SCENES[name]()
+    return _cache[name]
