@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Variant sweep on one GPU: same frame, several env settings, one process.
+Checks every variant's image is identical to the first (exactness guard)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zig_raytracing_contest_amd import camera_for, native, scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="cfg3")
+ap.add_argument("--spp", type=int, default=64)
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--var", action="append", default=[], help="ENV=VAL[,ENV=VAL] per variant")
+a = ap.parse_args()
+cfg = scenes.CONFIGS[a.config]
+soup = scenes.get_scene(cfg["scene"])
+cam = camera_for(soup, cfg["camera"], cfg["width"], cfg["height"])
+geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
+keep = []
+native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
+ref = None
+for var in (a.var or [""]):
+    env = dict(kv.split("=") for kv in var.split(",") if kv)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    ctx = native.Context(geo.scene)
+    img = np.zeros((cam.h, cam.w, 3), np.uint8)
+    ctx.render(cam, a.spp, cfg["max_bounce"], image=img)   # warm
+    ts = []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        r = ctx.render(cam, a.spp, cfg["max_bounce"], image=img)
+        ts.append(time.perf_counter() - t0)
+    st = r["stats"]
+    same = True if ref is None else bool(np.array_equal(ref, img))
+    if ref is None:
+        ref = img.copy()
+    print(json.dumps({"var": var or "default", "mrays": round(st["segments"] / min(ts) / 1e6, 1),
+                      "kernel_ms": round(st["trace_kernel_ms"], 2), "wall_ms": round(min(ts) * 1e3, 2),
+                      "identical": same}), flush=True)
+    ctx.close()
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
