@@ -1,0 +1,275 @@
+// cli.cpp -- `zrt`, the drop-in for the reference executable (src/main.zig).
+//
+//   zrt [--in input.gltf] [--out output.png] [--camera NAME] [--width N] [--height N]
+//
+// Same flags and defaults as main.zig:33-39 (zig-args: `--flag value` or
+// `--flag=value`), config.json read from the working directory with the same
+// keys (main.zig:56-69: grid_resolution, num_threads, num_samples,
+// max_bounce), the same phase log lines on stderr ("info: Loaded in ...",
+// main.zig:103-142, durations printed like std.fmt.fmtDuration).  The render
+// phase runs the HIP path on every GPU listed in ZRT_DEVICES (default: device
+// 0); several GPUs split the image into interleaved tiles, one context each.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/zrt.h"
+#include "json.h"
+
+extern "C" int zrt_png_write(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h);
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+// std.fmt.fmtDuration (Zig 0.11)
+std::string fmt_duration(uint64_t ns) {
+    std::string out;
+    const struct { uint64_t ns; const char* sep; } big[] = {
+        {365ull * 86400 * 1000000000ull, "y"}, {7ull * 86400 * 1000000000ull, "w"},
+        {86400ull * 1000000000ull, "d"}, {3600ull * 1000000000ull, "h"}, {60ull * 1000000000ull, "m"}};
+    for (const auto& u : big) {
+        if (ns >= u.ns) {
+            const uint64_t n = ns / u.ns;
+            out += std::to_string(n) + u.sep;
+            ns -= n * u.ns;
+            if (ns == 0) return out;
+        }
+    }
+    const struct { uint64_t ns; const char* sep; } small[] = {
+        {1000000000ull, "s"}, {1000000ull, "ms"}, {1000ull, "us"}};
+    for (const auto& u : small) {
+        const uint64_t k = ns * 1000 / u.ns;
+        if (k >= 1000) {
+            out += std::to_string(k / 1000);
+            const uint64_t frac = k % 1000;
+            if (frac) {
+                char buf[8];
+                snprintf(buf, sizeof buf, ".%03llu", (unsigned long long)frac);
+                std::string f(buf);
+                while (f.size() > 1 && f.back() == '0') f.pop_back();
+                out += f;
+            }
+            return out + u.sep;
+        }
+    }
+    return out + std::to_string(ns) + "ns";
+}
+
+uint64_t since(Clock::time_point t) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t).count();
+}
+
+void info(const std::string& s) { fprintf(stderr, "info: %s\n", s.c_str()); }
+int fail(const char* what, int rc) {
+    fprintf(stderr, "error: %s: %s\n", what, zrt_error_string(rc));
+    return 1;
+}
+
+struct Config {
+    uint32_t res[3] = {128, 128, 128};
+    int num_threads = -1;   // null
+    uint32_t num_samples = 3, max_bounce = 4;
+};
+
+bool load_config(const char* path, Config* c, std::string* err) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { *err = "FileNotFound: config.json"; return false; }
+    std::string s;
+    char buf[4096];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+    fclose(f);
+    zrt::json::Value v;
+    if (!zrt::json::parse(s.data(), s.size(), &v) || v.type != zrt::json::Value::Object) {
+        *err = "SyntaxError in config.json";
+        return false;
+    }
+    for (const auto& kv : v.obj) {   // std.json rejects unknown fields
+        if (kv.first != "grid_resolution" && kv.first != "num_threads" && kv.first != "num_samples" &&
+            kv.first != "max_bounce") {
+            *err = "UnknownField: " + kv.first;
+            return false;
+        }
+    }
+    const zrt::json::Value* g = v.get("grid_resolution");
+    if (!g || g->type != zrt::json::Value::Array || g->size() != 3) { *err = "MissingField: grid_resolution"; return false; }
+    for (int i = 0; i < 3; ++i) c->res[i] = (uint32_t)(*g)[i].num;
+    const zrt::json::Value* t = v.get("num_threads");
+    c->num_threads = (t && t->type == zrt::json::Value::Number) ? (int)t->num : -1;
+    if (!v.get("num_samples") || !v.get("max_bounce")) { *err = "MissingField"; return false; }
+    c->num_samples = (uint32_t)v.number("num_samples", 3);
+    c->max_bounce = (uint32_t)v.number("max_bounce", 4);
+    return true;
+}
+
+void usage() {
+    fprintf(stderr,
+            "usage: zrt [--in input.gltf] [--out output.png] [--camera NAME] [--width N] [--height N]\n"
+            "  config.json (cwd): grid_resolution, num_threads, num_samples, max_bounce\n"
+            "  ZRT_DEVICES=0,1,...  GPUs to render on (image tiles split across them)\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const auto t_start = Clock::now();
+    std::string in = "input.gltf", out = "output.png";
+    const char* camera = nullptr;
+    std::string camera_s;
+    int width = -1, height = -1;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i], val;
+        const size_t eq = a.find('=');
+        bool has_val = false;
+        if (a.rfind("--", 0) == 0 && eq != std::string::npos) { val = a.substr(eq + 1); a = a.substr(0, eq); has_val = true; }
+        auto next = [&]() -> bool {
+            if (has_val) return true;
+            if (i + 1 >= argc) return false;
+            val = argv[++i];
+            return true;
+        };
+        if (a == "--help" || a == "-h") { usage(); return 0; }
+        if (a != "--in" && a != "--out" && a != "--camera" && a != "--width" && a != "--height") {
+            fprintf(stderr, "error: unknown option %s\n", a.c_str());
+            usage();
+            return 1;
+        }
+        if (!next()) { fprintf(stderr, "error: missing value for %s\n", a.c_str()); return 1; }
+        if (a == "--in") in = val;
+        else if (a == "--out") out = val;
+        else if (a == "--camera") { camera_s = val; camera = camera_s.c_str(); }
+        else {
+            char* e = nullptr;
+            const long v = strtol(val.c_str(), &e, 10);
+            if (!e || *e || v < 0 || v > 65535) { fprintf(stderr, "error: %s must be u16\n", a.c_str()); return 1; }
+            (a == "--width" ? width : height) = (int)v;
+        }
+    }
+    Config cfg;
+    std::string err;
+    if (!load_config("config.json", &cfg, &err)) { fprintf(stderr, "error: %s\n", err.c_str()); return 1; }
+    info("Num samples: " + std::to_string(cfg.num_samples) + ", max bounce " + std::to_string(cfg.max_bounce));
+    const uint32_t num_threads = cfg.num_threads >= 0 ? (uint32_t)cfg.num_threads
+                                                      : std::max(1u, std::thread::hardware_concurrency());
+    info("Num threads: " + std::to_string(num_threads));
+
+    // GPUs
+    std::vector<int> devices;
+    if (const char* e = getenv("ZRT_DEVICES")) {
+        std::string s(e);
+        size_t p = 0;
+        while (p < s.size()) {
+            const size_t q = s.find(',', p);
+            devices.push_back(atoi(s.substr(p, q == std::string::npos ? std::string::npos : q - p).c_str()));
+            if (q == std::string::npos) break;
+            p = q + 1;
+        }
+    }
+    if (devices.empty()) devices.push_back(0);
+
+    zrt_scene scene;
+    memset(&scene, 0, sizeof scene);
+    zrt_camera cam;
+    zrt_gltf* gltf = nullptr;
+    zrt_geometry* geo = nullptr;
+    int rc;
+    {
+        const auto t = Clock::now();
+        if ((rc = zrt_gltf_load(in.c_str(), num_threads, &gltf)) != ZRT_OK) return fail("loadGltfFile", rc);
+        info("Loaded in " + fmt_duration(since(t)));
+    }
+    const float *pos, *nrm, *uv;
+    const uint32_t* mat;
+    uint32_t ntri = 0;
+    {
+        const auto t = Clock::now();
+        if ((rc = zrt_gltf_camera(gltf, camera, width, height, &cam)) != ZRT_OK) return fail("loadCamera", rc);
+        info("Pixels count: " + std::to_string((uint64_t)cam.w * cam.h));
+        zrt_gltf_materials(gltf, &scene);
+        info("Materials count: " + std::to_string(scene.num_materials));
+        zrt_gltf_soup(gltf, &pos, &nrm, &uv, &mat, &ntri);
+        info("Preprocessed in " + fmt_duration(since(t)));
+    }
+    {
+        const auto t = Clock::now();
+        info("Grid resolution: { " + std::to_string(cfg.res[0]) + ", " + std::to_string(cfg.res[1]) + ", " +
+             std::to_string(cfg.res[2]) + " }");
+        if ((rc = zrt_geometry_build(pos, nrm, uv, mat, ntri, cfg.res, num_threads, &geo)) != ZRT_OK)
+            return fail("Geometry.build", rc);
+        zrt_geometry_scene(geo, &scene);
+        uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0;
+        for (uint32_t c = 0; c < scene.num_cells; ++c) {
+            const uint32_t k = scene.cells[2 * c + 1] - scene.cells[2 * c];
+            if (!k) ++empty;
+            else { mn = std::min(mn, k); mx = std::max(mx, k); }
+        }
+        char buf[256];
+        const uint32_t nonempty = scene.num_cells - empty;
+        snprintf(buf, sizeof buf, "Empty cells: %u/%u (%.2f%%) min triangles: %u max triangles: %u mean_triangles: %u",
+                 empty, scene.num_cells, 100.0 * empty / scene.num_cells, nonempty ? mn : 0xFFFFFFFFu, mx,
+                 nonempty ? scene.num_triangles / nonempty : 0);
+        info(buf);
+        snprintf(buf, sizeof buf, "Unique triangle count: %u/%u (%.2f%%)", ntri, scene.num_triangles,
+                 scene.num_triangles ? 100.0 * ntri / scene.num_triangles : 0.0);
+        info(buf);
+        info("Compiled in " + fmt_duration(since(t)));
+    }
+    std::vector<zrt_context*> ctx(devices.size(), nullptr);
+    {
+        const auto t = Clock::now();
+        std::vector<int> rcs(devices.size(), ZRT_OK);
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devices.size(); ++i)
+            th.emplace_back([&, i] { rcs[i] = zrt_context_create(&scene, devices[i], &ctx[i]); });
+        for (auto& x : th) x.join();
+        for (int r : rcs)
+            if (r != ZRT_OK) return fail("zrt_context_create", r);
+        info("Uploaded in " + fmt_duration(since(t)));
+    }
+    std::vector<uint8_t> img((size_t)cam.w * cam.h * 3, 0);
+    {
+        const auto t = Clock::now();
+        std::vector<int> rcs(devices.size(), ZRT_OK);
+        std::vector<zrt_stats> st(devices.size());
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devices.size(); ++i)
+            th.emplace_back([&, i] {
+                zrt_render_config rc_{};
+                rc_.num_samples = cfg.num_samples;
+                rc_.max_bounce = cfg.max_bounce;
+                rc_.device = devices[i];
+                rc_.rank = (uint32_t)i;
+                rc_.num_ranks = (uint32_t)devices.size();
+                zrt_outputs o{};
+                o.rgb_image = img.data();   // disjoint pixels per rank
+                rcs[i] = zrt_context_render(ctx[i], &cam, &rc_, &o, &st[i]);
+            });
+        for (auto& x : th) x.join();
+        for (int r : rcs)
+            if (r != ZRT_OK) return fail("Scene.render", r);
+        const uint64_t ns = since(t);
+        uint64_t seg = 0;
+        for (const auto& s : st) seg += s.segments;
+        info("Rendered in " + fmt_duration(ns));
+        char buf[160];
+        snprintf(buf, sizeof buf, "Rays: %llu segments, %.1f Mrays/s on %zu GPU(s)", (unsigned long long)seg,
+                 seg / (ns / 1e9) / 1e6, devices.size());
+        info(buf);
+    }
+    for (zrt_context* c : ctx) zrt_context_destroy(c);
+    {
+        const auto t = Clock::now();
+        if ((rc = zrt_png_write(out.c_str(), img.data(), cam.w, cam.h)) != ZRT_OK) return fail("WritePngFail", rc);
+        info("Saved in " + fmt_duration(since(t)));
+    }
+    zrt_geometry_free(geo);
+    zrt_gltf_free(gltf);
+    info("Done in " + fmt_duration(since(t_start)));
+    return 0;
+}

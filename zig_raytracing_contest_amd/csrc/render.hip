@@ -50,7 +50,9 @@ using namespace zrt;
 namespace {
 
 constexpr float kFltEps = 1.1920928955078125e-07f;   // std.math.floatEps(f32)
-constexpr int kBlock = 256;                          // 4 waves
+constexpr int kBlock = 256;                          // resolve / probes
+constexpr int kTraceBlock = 512;                     // launch bound; launched with trace_block()
+constexpr int kTriBatch = 2;                         // triangle loads in flight per lane
 
 struct TraceParams {
     float bmin[3], bmax[3];
@@ -64,8 +66,6 @@ struct TraceParams {
     const double* zig;        // zx[257], zf[257]
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
-    const uint32_t* occ4;     // v4 LDS blob: brick bits | prefix counts | u64 cell masks
-    uint32_t occ4_words, occ4_nbw, occ4_nb0, occ4_nb01;
     float org[3], llc[3], right[3], up[3];
     uint32_t w;
     const uint32_t* pixlist;
@@ -73,36 +73,39 @@ struct TraceParams {
     uint32_t s0;              // first sample index of this pass
     uint32_t total;           // items in this pass
     uint32_t max_bounce;
-    uint32_t chunk;           // v3: items per wave-level fetch
-    uint32_t shade_min;       // v3: lanes waiting before a shading phase
     uint64_t seed;
     float4* out;              // total
     uint32_t* counter;
-    unsigned long long* stats;   // segments, cells, tests, hits
+    unsigned long long* stats;   // segments, cells, tests, hits | profile
 };
 
-// per-bounce (emissive, albedo) pairs in registers; identity = (0, 1) so that
-// pass-through bounces and unused slots fold as e + a*L = L exactly.
+// Per-bounce (emissive, albedo) pairs of one path.  The fold reads them back
+// to front: e0 + a0*(e1 + a1*(...)) is traceRayRecursive's arithmetic
+// (stage3.zig:219); pass-through bounces (stage3.zig:212) add no pair.  The
+// array is indexed by the bounce slot at run time, so it lives in scratch
+// memory: it is written once per scatter and read once per path, never in
+// the traversal loop, and keeping it out of VGPRs buys waves per SIMD.
 template <int N>
 struct Stack {
-    v3 e[N], a[N];
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int i = 0; i < N; ++i) { e[i] = mk(0, 0, 0); a[i] = mk(1, 1, 1); }
-    }
+    float e[3 * N], a[3 * N];
+    uint32_t used;
+    __device__ __forceinline__ void init() { used = 0u; }
     __device__ __forceinline__ void set(uint32_t slot, v3 ee, v3 aa) {
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if ((uint32_t)i == slot) { e[i] = ee; a[i] = aa; }
+        e[3 * slot] = ee.x; e[3 * slot + 1] = ee.y; e[3 * slot + 2] = ee.z;
+        a[3 * slot] = aa.x; a[3 * slot + 1] = aa.y; a[3 * slot + 2] = aa.z;
+        used |= 1u << slot;
     }
     __device__ __forceinline__ v3 fold(v3 L) const {
-#pragma unroll
-        for (int i = N - 1; i >= 0; --i) L = add(e[i], mul(a[i], L));
+        for (int i = N - 1; i >= 0; --i) {
+            if ((used >> i) & 1u) {
+                L = add(mk(e[3 * i], e[3 * i + 1], e[3 * i + 2]),
+                        mul(mk(a[3 * i], a[3 * i + 1], a[3 * i + 2]), L));
+            }
+        }
         return L;
     }
 };
 
-// Scene.traceRay (stage3.zig:152-186): nearest hit along the grid DDA.
 __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint32_t* occ, uint32_t c0,
                                                uint32_t c1, uint32_t c2) {
     const uint32_t s = p.occ_shift;
@@ -110,14 +113,14 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
-// Grid.Iterator state (linalg.zig:471-477) + the running cell index.
+// Grid.Iterator state (linalg.zig:471-477) + the running cell index.  The
+// exit cell, step and linear-index step of each axis follow from the sign of
+// the ray direction (linalg.zig:450-452), kept as 3 bits in `neg`.
 struct Dda {
     float tn0, tn1, tn2, td0, td1, td2;
-    uint32_t c0, c1, c2;          // cell
-    uint32_t e0, e1, e2;          // exit cell per axis
-    uint32_t s0, s1, s2;          // step: 1 or 0xFFFFFFFF (wrapping add, linalg.zig:492)
-    uint32_t dl0, dl1, dl2;       // matching step of the linear cell index
+    uint32_t c0, c1, c2;
     uint32_t lin;
+    uint32_t neg;             // bit a: dir[a] < 0
 };
 
 // Grid.traceRay (linalg.zig:443-469); false if the ray misses the grid bbox.
@@ -129,27 +132,18 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
     if (!bbox_ray(bb, o, d, &t_hit)) return false;
     t_hit = fmaxf(0.0f, t_hit);
     const v3 local = sub(add(o, scale(d, t_hit)), bb.min);
-    const uint32_t rx = p.res[0], rxy = p.res[0] * p.res[1];
     const bool n0 = d.x < 0.0f, n1 = d.y < 0.0f, n2 = d.z < 0.0f;
     s.c0 = min(f2u(local.x / p.cs[0]), p.res[0] - 1u);
     s.c1 = min(f2u(local.y / p.cs[1]), p.res[1] - 1u);
     s.c2 = min(f2u(local.z / p.cs[2]), p.res[2] - 1u);
-    s.e0 = n0 ? 0u : p.res[0] - 1u;
-    s.e1 = n1 ? 0u : p.res[1] - 1u;
-    s.e2 = n2 ? 0u : p.res[2] - 1u;
-    s.s0 = n0 ? 0xFFFFFFFFu : 1u;
-    s.s1 = n1 ? 0xFFFFFFFFu : 1u;
-    s.s2 = n2 ? 0xFFFFFFFFu : 1u;
-    s.dl0 = n0 ? 0xFFFFFFFFu : 1u;
-    s.dl1 = n1 ? 0u - rx : rx;
-    s.dl2 = n2 ? 0u - rxy : rxy;
+    s.neg = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
     s.td0 = fabsf(p.cs[0] / d.x);
     s.td1 = fabsf(p.cs[1] / d.y);
     s.td2 = fabsf(p.cs[2] / d.z);
     s.tn0 = t_hit + ((((float)(s.c0 + (n0 ? 0u : 1u))) * p.cs[0] - local.x) / d.x);
     s.tn1 = t_hit + ((((float)(s.c1 + (n1 ? 0u : 1u))) * p.cs[1] - local.y) / d.y);
     s.tn2 = t_hit + ((((float)(s.c2 + (n2 ? 0u : 1u))) * p.cs[2] - local.z) / d.z);
-    s.lin = s.c2 * rxy + s.c1 * rx + s.c0;
+    s.lin = (s.c2 * p.res[1] + s.c1) * p.res[0] + s.c0;
     return true;
 }
 
@@ -160,10 +154,10 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
 // the chosen axis, or +inf at the exit cell.  On that +inf the state is
 // stepped past the exit, which is harmless: traceRay always stops there
 // (nearest <= inf).  CROSSED: the step left the current occupancy brick.
-// A macro over a local Dda (not a function on a reference): as a function,
+// A macro over a local Dda, not a function on a reference: as a function,
 // InstCombine turns `a0 ? s.c0 : s.c1` into a load through a selected
 // pointer and the whole state lands in scratch memory.
-#define DDA_STEP(S, SH, CROSSED, T_EXIT)                                              \
+#define DDA_STEP(S, P, SH, CROSSED, T_EXIT)                                           \
     do {                                                                             \
         const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
         const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
@@ -173,10 +167,12 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
         const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
         const uint32_t c0_ = (S).c0, c1_ = (S).c1, c2_ = (S).c2;                     \
         const uint32_t cc_ = a0_ ? c0_ : (a1_ ? c1_ : c2_);                          \
-        const uint32_t ec_ = a0_ ? (S).e0 : (a1_ ? (S).e1 : (S).e2);                 \
-        const uint32_t sc_ = a0_ ? (S).s0 : (a1_ ? (S).s1 : (S).s2);                 \
-        const uint32_t dl_ = a0_ ? (S).dl0 : (a1_ ? (S).dl1 : (S).dl2);              \
-        const uint32_t cn_ = cc_ + sc_;                                              \
+        const uint32_t ax_ = a0_ ? 0u : (a1_ ? 1u : 2u);                             \
+        const bool ng_ = ((S).neg >> ax_) & 1u;                                      \
+        const uint32_t rm1_ = (a0_ ? (P).res[0] : (a1_ ? (P).res[1] : (P).res[2])) - 1u; \
+        const uint32_t ec_ = ng_ ? 0u : rm1_;                                        \
+        const uint32_t cn_ = ng_ ? cc_ - 1u : cc_ + 1u;                              \
+        const uint32_t str_ = a0_ ? 1u : (a1_ ? (P).res[0] : (P).res[0] * (P).res[1]); \
         (CROSSED) = ((cc_ ^ cn_) >> (SH)) != 0u;                                     \
         const float u0_ = t0_ + (S).td0, u1_ = t1_ + (S).td1, u2_ = t2_ + (S).td2;   \
         (S).tn0 = a0_ ? u0_ : t0_;                                                   \
@@ -185,24 +181,13 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
         (S).c0 = a0_ ? cn_ : c0_;                                                    \
         (S).c1 = a1_ ? cn_ : c1_;                                                    \
         (S).c2 = a2_ ? cn_ : c2_;                                                    \
-        (S).lin += dl_;                                                              \
+        (S).lin = ng_ ? (S).lin - str_ : (S).lin + str_;                             \
         (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
     } while (0)
 
-__device__ __forceinline__ void tri_test(const TraceParams& p, uint32_t i, v3 o, v3 d, float& nearest,
-                                         float& hu, float& hv, uint32_t& hidx) {
-    const float4 a = p.tri_pos[3 * i + 0];
-    const float4 b = p.tri_pos[3 * i + 1];
-    const float4 cc = p.tri_pos[3 * i + 2];
-    float t, u, v;
-    if (tri_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(cc.x, cc.y, cc.z), o, d, &t, &u, &v)) {
-        if (nearest > t && t > 0.0f) { nearest = t; hu = u; hv = v; hidx = i; }   // stage3.zig:174
-    }
-}
-
-// All triangles of one cell in reference order, TB at a time: the TB loads
-// are issued before the first test so their latencies overlap (the loop of
-// tri_test waits one memory round trip per triangle).
+// All triangles of one cell in reference order (stage3.zig:164-178), TB at
+// a time: the TB loads are issued before the first test so their latencies
+// overlap (one memory round trip per TB triangles instead of per triangle).
 template <int TB, bool STATS>
 __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
                                           float& nearest, float& hu, float& hv, uint32_t& hidx,
@@ -242,10 +227,10 @@ __device__ __forceinline__ uint64_t stamp() {
 // nothing in the result: the DDA arithmetic runs for every cell exactly as
 // Iterator.next does; only the 8-byte Cell load is skipped when the cell's
 // brick holds no triangle (its range would be empty).
-template <bool STATS, bool PROF = false, int TB = 1>
+template <bool STATS, bool PROF, int TB>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
-                                           uint32_t& n_tests, uint64_t* prof = nullptr) {
+                                           uint32_t& n_tests, uint64_t* prof) {
     float nearest = kInf;
     Dda s;
     if (!dda_setup(p, o, d, s)) return nearest;
@@ -262,77 +247,10 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         if (PROF) tb = stamp();
         bool crossed;
         float t_exit;
-        DDA_STEP(s, sh, crossed, t_exit);
-        if (nearest <= t_exit) break;
+        DDA_STEP(s, p, sh, crossed, t_exit);
+        if (nearest <= t_exit) break;                      // stage3.zig:179-182
         if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
         if (PROF) { const uint64_t tc = stamp(); prof[0] += tb - ta; prof[1] += tc - tb; }
-    }
-    return nearest;
-}
-
-// ---------------------------------------------------------------------------
-// v4 tracer: exact per-cell occupancy from LDS + run-ahead.
-//
-// LDS holds, for 4x4x4-cell bricks: one bit per brick, the number of set bits
-// before each 32-bit word, and one 64-bit cell mask per OCCUPIED brick.  An
-// empty cell therefore costs DDA arithmetic + (on brick entry) three LDS
-// reads, never a global load.  Triangles are tested cell by cell in the
-// reference order; while a cell's range load is in flight the DDA runs ahead
-// to the next non-empty cell, remembering the largest exit t it passed:
-// after the current cell's tests the reference breaks at the first passed
-// cell j with nearest <= t_exit(j); nearest is constant across those empty
-// cells, so "some j breaks" <=> nearest <= max_j t_exit(j) (fmaxf skips NaN
-// exactly as `<=` against NaN is false).  The run-ahead may stop as soon as
-// the PRE-test nearest already satisfies nearest <= t_exit: tests can only
-// lower it.  Same cells, same tests, same order, same hit.
-struct Occ4 {
-    const uint32_t* bits;
-    const uint32_t* prefix;
-    const uint64_t* masks;
-};
-
-__device__ __forceinline__ uint64_t brick_mask4(const TraceParams& p, const Occ4& L, uint32_t c0,
-                                                uint32_t c1, uint32_t c2) {
-    const uint32_t b = (c2 >> 2) * p.occ4_nb01 + (c1 >> 2) * p.occ4_nb0 + (c0 >> 2);
-    const uint32_t w = L.bits[b >> 5];
-    const uint32_t bit = 1u << (b & 31u);
-    const uint32_t r = L.prefix[b >> 5] + (uint32_t)__popc(w & (bit - 1u));
-    const uint64_t m = L.masks[r];          // masks has one zero entry of padding
-    return (w & bit) ? m : 0ull;
-}
-__device__ __forceinline__ uint32_t cell_bit4(uint32_t c0, uint32_t c1, uint32_t c2) {
-    return ((c2 & 3u) << 4) | ((c1 & 3u) << 2) | (c0 & 3u);
-}
-
-__device__ __forceinline__ float trace_ray_v4(const TraceParams& p, const Occ4& L, v3 o, v3 d,
-                                              float& hu, float& hv, uint32_t& hidx) {
-    float nearest = kInf;
-    Dda s;
-    if (!dda_setup(p, o, d, s)) return nearest;
-    uint64_t bm = brick_mask4(p, L, s.c0, s.c1, s.c2);
-    uint2 cur = make_uint2(0u, 0u);
-    bool found = (bm >> cell_bit4(s.c0, s.c1, s.c2)) & 1ull;
-    float tmax = -kInf;
-    for (;;) {
-        if (found) cur = p.cells[s.lin];
-        // run ahead to the next non-empty cell
-        found = false;
-        tmax = -kInf;
-        for (;;) {
-            bool crossed;
-            float t_exit;
-            DDA_STEP(s, 2u, crossed, t_exit);
-            tmax = fmaxf(tmax, t_exit);
-            if (nearest <= t_exit) break;
-            if (crossed) bm = brick_mask4(p, L, s.c0, s.c1, s.c2);
-            if ((bm >> cell_bit4(s.c0, s.c1, s.c2)) & 1ull) { found = true; break; }
-        }
-        uint2 nxt = make_uint2(0u, 0u);
-        if (found) nxt = p.cells[s.lin];
-        for (uint32_t i = cur.x; i < cur.y; ++i) tri_test(p, i, o, d, nearest, hu, hv, hidx);
-        if (nearest <= tmax) break;
-        cur = nxt;
-        found = false;
     }
     return nearest;
 }
@@ -362,32 +280,22 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
-template <int MAXB, bool STATS, int VER, int BLOCK, bool PROF = false, int TB = 1>
-__global__ __launch_bounds__(BLOCK) void trace_kernel(const TraceParams p) {
-    uint64_t prof[6] = {0, 0, 0, 0, 0, 0};   // cell+tris, dda, trace, shade, fetch, total
-    const uint64_t t_begin = PROF ? stamp() : 0;
+// The path-trace kernel: renderWorker's per-sample body (stage3.zig:237-241)
+// + traceRayRecursive (stage3.zig:188-220) made iterative.
+template <int MAXB, bool STATS, bool PROF, int TB, int MINW>
+__global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TraceParams p) {
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    for (int i = threadIdx.x; i < 514; i += BLOCK) s_zig[i] = p.zig[i];
-    if (VER == 4) {
-        for (uint32_t i = threadIdx.x; i < p.occ4_words; i += BLOCK) s_occ[i] = p.occ4[i];
-    } else {
-        for (uint32_t i = threadIdx.x; i < p.occ_words; i += BLOCK) s_occ[i] = p.occ[i];
-    }
+    uint64_t prof[6] = {0, 0, 0, 0, 0, 0};   // cell+tris, dda, trace, shade, fetch, total
+    const uint64_t t_begin = PROF ? stamp() : 0;
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
     __syncthreads();
-    Occ4 L4;
-    L4.bits = s_occ;
-    L4.prefix = s_occ + p.occ4_nbw;
-    L4.masks = (const uint64_t*)(s_occ + 2 * p.occ4_nbw);
     const double* zx = s_zig;
     const double* zf = s_zig + 257;
 
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
-    const v3 org = mk(p.org[0], p.org[1], p.org[2]);
-    const v3 llc = mk(p.llc[0], p.llc[1], p.llc[2]);
-    const v3 right = mk(p.right[0], p.right[1], p.right[2]);
-    const v3 up = mk(p.up[0], p.up[1], p.up[2]);
 
     for (;;) {
         const uint64_t t_fetch = PROF ? stamp() : 0;
@@ -400,18 +308,18 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(const TraceParams p) {
 
         const uint32_t s_local = item / p.P;
         const uint32_t q = item - s_local * p.P;
-        const uint32_t sample = p.s0 + s_local;
         const uint32_t pixel = p.pixlist[q];
         const uint32_t py = pixel / p.w;
         const uint32_t px = pixel - py * p.w;
         Rng rng;
-        rng.s = path_key(p.seed, pixel, sample);
+        rng.s = path_key(p.seed, pixel, p.s0 + s_local);
         // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35)
         const float jx = rng_float(rng);
         const float jy = rng_float(rng);
-        v3 o = org;
-        v3 d = normalize(add(add(llc, scale(right, (float)px + jx)), scale(up, (float)py + jy)));
-
+        v3 o = mk(p.org[0], p.org[1], p.org[2]);
+        v3 d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
+                                 scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
+                             scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
         Stack<MAXB> stk;
         stk.init();
         v3 L = mk(0, 0, 0);
@@ -421,17 +329,15 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(const TraceParams p) {
             ++n_seg;
             float hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
-            float t;
             const uint64_t t_tr = PROF ? stamp() : 0;
-            if (VER == 4 && !STATS) t = trace_ray_v4(p, L4, o, d, hu, hv, hidx);
-            else t = trace_ray<STATS, PROF, TB>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof);
+            const float t = trace_ray<STATS, PROF, TB>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof);
             const uint64_t t_sh = PROF ? stamp() : 0;
             if (PROF) prof[2] += t_sh - t_tr;
             if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
             if (STATS) ++n_hits;
             // stage3.zig:199-206
-            const float4* td = p.tri_data + 4ull * hidx;
-            const float4 d0 = td[0], d1 = td[1], d2 = td[2], d3 = td[3];
+            const float4* tdp = p.tri_data + 4ull * hidx;
+            const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
             const float w0 = 1.0f - hu - hv;
             const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
             const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
@@ -442,17 +348,15 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(const TraceParams p) {
             const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
                                scale(mk(d1.z, d1.w, d2.x), hv));
             const v3 no = add(o, scale(d, t + kFltEps));        // ray.at(hit.t + eps)
-            if (rng_float(rng) > transparency) {                // stage3.zig:207-213
-                o = no;
-                continue;
-            }
-            // randomUnitVector (linalg.zig:140-148): 3 x floatNorm, normalize
-            const float nx = (float)rng_norm64(rng, zx, zf);
-            const float ny = (float)rng_norm64(rng, zx, zf);
-            const float nz = (float)rng_norm64(rng, zx, zf);
-            d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+            if (!(rng_float(rng) > transparency)) {             // stage3.zig:207
+                // randomUnitVector (linalg.zig:140-148): 3 x floatNorm, normalize
+                const float nx = (float)rng_norm64(rng, zx, zf);
+                const float ny = (float)rng_norm64(rng, zx, zf);
+                const float nz = (float)rng_norm64(rng, zx, zf);
+                d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+                stk.set(slot, emissive, albedo);                // stage3.zig:214-219
+            }                                                   // else pass-through :208-212
             o = no;
-            stk.set(slot, emissive, albedo);                    // stage3.zig:219
             if (PROF) prof[3] += stamp() - t_sh;
         }
         L = stk.fold(L);
@@ -462,191 +366,6 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(const TraceParams p) {
         prof[5] = stamp() - t_begin;
         if (lane == 0)
             for (int k = 0; k < 6; ++k) atomicAdd(&p.stats[8 + k], (unsigned long long)prof[k]);
-    }
-    const unsigned long long s0 = wave_sum(n_seg);
-    unsigned long long s1 = 0, s2 = 0, s3 = 0;
-    if (STATS) { s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits); }
-    if (lane == 0) {
-        atomicAdd(&p.stats[0], s0);
-        if (STATS) {
-            atomicAdd(&p.stats[1], s1);
-            atomicAdd(&p.stats[2], s2);
-            atomicAdd(&p.stats[3], s3);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// v3: per-lane path state machine with lane refill.
-//
-// trace_kernel above runs one path per lane start to finish, so a wave lives
-// as long as its longest path and its longest DDA walk: measured VALU lane
-// utilisation ~19% on cfg3.  Here every lane is a small state machine
-// (IDLE -> TRAV -> SHADE -> TRAV ... -> IDLE) and a wave loops over three
-// phases (Aila & Laine's persistent while-while with dynamic fetch):
-//   refill    IDLE lanes take the next items from a wave-local chunk (one
-//             global atomic per `chunk` items, ballot + mbcnt ranks);
-//   traverse  lanes ADVANCE through cells until one holds triangles (pure DDA
-//             arithmetic + LDS brick bits; postponed intersection), then all
-//             lanes with pending triangles INTERSECT them; repeat until at
-//             least `shade_min` lanes wait for shading or none traverses;
-//   shade     lanes whose segment ended shade, bounce (new segment) or fold
-//             their stack, write the sample and go IDLE.
-// Every per-ray operation and its order is that of trace_kernel, so the
-// radiance of each sample is unchanged bit for bit.
-enum : uint32_t { ST_IDLE = 0, ST_TRAV = 1, ST_SHADE = 2 };
-
-template <int MAXB, bool STATS>
-__global__ __launch_bounds__(kBlock) void trace_kernel_v3(const TraceParams p) {
-    __shared__ double s_zig[514];
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    for (int i = threadIdx.x; i < 514; i += kBlock) s_zig[i] = p.zig[i];
-    for (uint32_t i = threadIdx.x; i < p.occ_words; i += kBlock) s_occ[i] = p.occ[i];
-    __syncthreads();
-    const double* zx = s_zig;
-    const double* zf = s_zig + 257;
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
-    uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
-    const uint32_t sh = p.occ_shift;
-
-    // wave-uniform work queue
-    uint32_t q_next = 0, q_end = 0;
-    bool exhausted = false;
-
-    // lane state
-    uint32_t state = ST_IDLE;
-    uint32_t item = 0, depth = 0, slot = 0;
-    Rng rng;
-    rng.s = 0;
-    Stack<MAXB> stk;
-    stk.init();
-    v3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-    Dda dd = {};
-    bool occupied = false;
-    float nearest = kInf, hu = 0.0f, hv = 0.0f;
-    uint32_t hidx = 0, ti = 0, te = 0;
-
-    // Grid.traceRay (linalg.zig:443-469) + first Cell load; sets TRAV or SHADE
-    auto start_segment = [&]() {
-        ++n_seg;
-        nearest = kInf;
-        ti = te = 0;
-        if (!dda_setup(p, o, d, dd)) { state = ST_SHADE; return; }
-        occupied = brick_occupied(p, s_occ, dd.c0, dd.c1, dd.c2);
-        if (STATS) ++n_cells;
-        if (occupied) { const uint2 cl = p.cells[dd.lin]; ti = cl.x; te = cl.y; }
-        state = ST_TRAV;
-    };
-    auto finish = [&](v3 L) {
-        L = stk.fold(L);
-        p.out[item] = make_float4(L.x, L.y, L.z, 0.0f);
-        state = ST_IDLE;
-    };
-
-    for (;;) {
-        // ---------------- refill ----------------
-        uint64_t need = __ballot(state == ST_IDLE);
-        while (need != 0ull && !exhausted) {
-            if (q_next == q_end) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(p.counter, p.chunk);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (base >= p.total) { exhausted = true; break; }
-                q_next = base;
-                q_end = min(base + p.chunk, p.total);
-            }
-            const uint32_t avail = q_end - q_next;
-            const uint32_t rank = (uint32_t)__popcll(need & below);
-            const uint32_t take = min(avail, (uint32_t)__popcll(need));
-            if (state == ST_IDLE && rank < take) {
-                item = q_next + rank;
-                const uint32_t s_local = item / p.P;
-                const uint32_t q = item - s_local * p.P;
-                const uint32_t pixel = p.pixlist[q];
-                const uint32_t py = pixel / p.w;
-                const uint32_t px = pixel - py * p.w;
-                rng.s = path_key(p.seed, pixel, p.s0 + s_local);
-                const float jx = rng_float(rng);
-                const float jy = rng_float(rng);
-                o = mk(p.org[0], p.org[1], p.org[2]);
-                d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
-                                      scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
-                                  scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
-                stk.init();
-                slot = 0;
-                depth = p.max_bounce;
-                if (depth == 0) finish(mk(0, 0, 0));
-                else start_segment();
-            }
-            q_next += take;
-            need = __ballot(state == ST_IDLE);
-        }
-        if (!__any(state != ST_IDLE)) break;
-
-        // ---------------- traverse ----------------
-        for (;;) {
-            if (!__any(state == ST_TRAV)) break;
-            // advance: DDA (Iterator.next) until a cell with triangles, or done
-            if (state == ST_TRAV && ti >= te) {
-                for (;;) {
-                    bool crossed;
-                    float t_exit;
-                    DDA_STEP(dd, sh, crossed, t_exit);
-                    if (nearest <= t_exit) { state = ST_SHADE; break; }   // stage3.zig:180-182
-                    if (STATS) ++n_cells;
-                    if (crossed) occupied = brick_occupied(p, s_occ, dd.c0, dd.c1, dd.c2);
-                    if (occupied) {
-                        const uint2 cl = p.cells[dd.lin];
-                        ti = cl.x;
-                        te = cl.y;
-                        if (ti < te) break;
-                    }
-                }
-            }
-            // intersect: every pending triangle of the current cell, in order
-            if (state == ST_TRAV) {
-                for (; ti < te; ++ti) {
-                    if (STATS) ++n_tests;
-                    tri_test(p, ti, o, d, nearest, hu, hv, hidx);
-                }
-            }
-            if ((uint32_t)__popcll(__ballot(state == ST_SHADE)) >= p.shade_min) break;
-        }
-
-        // ---------------- shade ----------------
-        if (state == ST_SHADE) {
-            if (nearest == kInf) {
-                finish(env_color(d));                               // stage3.zig:195-197
-            } else {
-                if (STATS) ++n_hits;
-                const float4* tdp = p.tri_data + 4ull * hidx;
-                const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
-                const float w0 = 1.0f - hu - hv;
-                const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
-                const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
-                const DevMat& m = p.mats[__float_as_uint(d3.w)];
-                const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
-                const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
-                const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
-                const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
-                                   scale(mk(d1.z, d1.w, d2.x), hv));
-                const v3 no = add(o, scale(d, nearest + kFltEps));
-                if (!(rng_float(rng) > transparency)) {
-                    const float nx = (float)rng_norm64(rng, zx, zf);
-                    const float ny = (float)rng_norm64(rng, zx, zf);
-                    const float nz = (float)rng_norm64(rng, zx, zf);
-                    d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
-                    stk.set(slot, emissive, albedo);
-                }
-                o = no;
-                --depth;
-                ++slot;
-                if (depth == 0) finish(mk(0, 0, 0));
-                else start_segment();
-            }
-        }
     }
     const unsigned long long s0 = wave_sum(n_seg);
     unsigned long long s1 = 0, s2 = 0, s3 = 0;
@@ -686,54 +405,37 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restric
 
 using TraceFn = void (*)(const TraceParams);
 
-int kernel_version() {
-    const char* e = getenv("ZRT_KERNEL");
-    return e ? atoi(e) : 4;
-}
-
-struct TraceKernel {
-    TraceFn fn = nullptr;
-    int block = kBlock;
-    int version = 2;
-};
-
 template <int MAXB>
-TraceKernel pick(bool stats, bool v4_ok) {
-    TraceKernel k;
-    const int ver = kernel_version();
-    if (getenv("ZRT_PROFILE")) {
-        k.fn = (TraceFn)trace_kernel<MAXB, false, 2, kBlock, true>;
-    } else if (stats) {   // exact per-cell counters: the reference-shaped loop
-        k.fn = (TraceFn)trace_kernel<MAXB, true, 2, kBlock>;
-    } else if (ver == 3) {
-        k.fn = (TraceFn)trace_kernel_v3<MAXB, false>;
-        k.version = 3;
-    } else if (ver == 4 && v4_ok) {
-        k.fn = (TraceFn)trace_kernel<MAXB, false, 4, 1024>;
-        k.block = 1024;
-        k.version = 4;
-    } else if (ver == 22) {
-        k.fn = (TraceFn)trace_kernel<MAXB, false, 2, kBlock, false, 2>;
-    } else if (ver == 24) {
-        k.fn = (TraceFn)trace_kernel<MAXB, false, 2, kBlock, false, 4>;
-    } else {
-        k.fn = (TraceFn)trace_kernel<MAXB, false, 2, kBlock>;
+TraceFn pick(bool stats, bool prof) {
+    if (prof) return (TraceFn)trace_kernel<MAXB, false, true, kTriBatch, 1>;
+    if (stats) return (TraceFn)trace_kernel<MAXB, true, false, kTriBatch, 1>;
+    if (MAXB == 4) {
+        const char* e = getenv("ZRT_MINW");
+        const int w = e ? atoi(e) : 0;
+        if (w == 3) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 3>;
+        if (w == 6) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 6>;
+        if (w == 8) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 8>;
     }
-    return k;
+    return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 1>;
 }
 
-TraceKernel trace_fn(uint32_t max_bounce, bool stats, bool v4_ok, int* maxb) {
-    if (max_bounce <= 4) { *maxb = 4; return pick<4>(stats, v4_ok); }
-    if (max_bounce <= 8) { *maxb = 8; return pick<8>(stats, v4_ok); }
-    if (max_bounce <= 16) { *maxb = 16; return pick<16>(stats, v4_ok); }
-    if (max_bounce <= 64) { *maxb = 64; return pick<64>(stats, v4_ok); }
-    return TraceKernel{};
+// Threads per trace block: a multiple of 64, at most the launch bound.
+int trace_block() {
+    int b = 256;
+    if (const char* e = getenv("ZRT_TRACE_BLOCK")) b = atoi(e);
+    b = std::max(64, std::min(kTraceBlock, b / 64 * 64));
+    return b;
 }
 
-uint32_t env_u32(const char* name, uint32_t dflt) {
-    const char* e = getenv(name);
-    return e ? (uint32_t)atoi(e) : dflt;
+// max_bounce picks the stack depth the kernel is compiled for.
+TraceFn trace_fn(uint32_t max_bounce, bool stats, bool prof) {
+    if (max_bounce <= 4) return pick<4>(stats, prof);
+    if (max_bounce <= 8) return pick<8>(stats, prof);
+    if (max_bounce <= 16) return pick<16>(stats, prof);
+    if (max_bounce <= 32) return pick<32>(stats, prof);
+    return nullptr;
 }
+
 
 struct DeviceGuard {
     int prev = -1;
@@ -774,9 +476,6 @@ struct zrt_context {
     double* d_zig = nullptr;
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
-    uint32_t* d_occ4 = nullptr;
-    uint32_t occ4_words = 0, occ4_nbw = 0, occ4_nb[3] = {0, 0, 0};
-    bool v4_ok = false;
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;
@@ -831,7 +530,7 @@ extern "C" int zrt_device_count(int* count) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occ4, c->d_pix,
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
                     c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -895,7 +594,7 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     // brick occupancy bitmap: smallest power-of-two brick whose bitmap fits
     // the LDS budget (ZRT_OCC_BYTES, default 32 KiB; ZRT_OCC_SHIFT forces it)
     {
-        size_t budget = 32768;
+        size_t budget = 4096;   // 4^3-cell bricks for a 128^3 grid (measured best, r01)
         if (const char* e = getenv("ZRT_OCC_BYTES")) budget = (size_t)atoll(e);
         int forced = -1;
         if (const char* e = getenv("ZRT_OCC_SHIFT")) forced = atoi(e);
@@ -925,45 +624,6 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
                 }
         HIP_TRY(hipMalloc((void**)&c->d_occ, bits.size() * 4));
         HIP_TRY(hipMemcpy(c->d_occ, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
-    }
-    // v4 blob: 4x4x4 bricks -> bits | prefix | u64 cell masks (+1 zero pad)
-    {
-        const uint32_t* r = s->grid.resolution;
-        for (int i = 0; i < 3; ++i) c->occ4_nb[i] = (r[i] + 3u) >> 2;
-        const uint64_t nb = (uint64_t)c->occ4_nb[0] * c->occ4_nb[1] * c->occ4_nb[2];
-        uint64_t nbw = (nb + 31) / 32;
-        nbw += nbw & 1;   // keep the u64 masks 8-byte aligned
-        std::vector<uint64_t> mask(nb, 0ull);
-        for (uint32_t z = 0; z < r[2]; ++z)
-            for (uint32_t y = 0; y < r[1]; ++y)
-                for (uint32_t x = 0; x < r[0]; ++x) {
-                    const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
-                    if (s->cells[2 * ci] < s->cells[2 * ci + 1]) {
-                        const uint64_t b = ((uint64_t)(z >> 2) * c->occ4_nb[1] + (y >> 2)) * c->occ4_nb[0] + (x >> 2);
-                        mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
-                    }
-                }
-        std::vector<uint32_t> bitsv(nbw, 0u), prefix(nbw, 0u);
-        std::vector<uint64_t> masks;
-        for (uint64_t b = 0; b < nb; ++b)
-            if (mask[b]) { bitsv[b >> 5] |= 1u << (b & 31); masks.push_back(mask[b]); }
-        uint32_t run = 0;
-        for (uint64_t w = 0; w < nbw; ++w) { prefix[w] = run; run += (uint32_t)__builtin_popcount(bitsv[w]); }
-        masks.push_back(0ull);
-        const uint64_t words = 2 * nbw + 2 * masks.size();
-        size_t budget = 150 * 1024 - 514 * 8;
-        if (const char* e = getenv("ZRT_LDS_BUDGET")) budget = (size_t)atoll(e);
-        c->v4_ok = words * 4 <= budget;
-        if (c->v4_ok) {
-            std::vector<uint32_t> blob(words);
-            memcpy(blob.data(), bitsv.data(), nbw * 4);
-            memcpy(blob.data() + nbw, prefix.data(), nbw * 4);
-            memcpy(blob.data() + 2 * nbw, masks.data(), masks.size() * 8);
-            c->occ4_words = (uint32_t)words;
-            c->occ4_nbw = (uint32_t)nbw;
-            HIP_TRY(hipMalloc((void**)&c->d_occ4, words * 4));
-            HIP_TRY(hipMemcpy(c->d_occ4, blob.data(), words * 4, hipMemcpyHostToDevice));
-        }
     }
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
@@ -1004,11 +664,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (cam->w == 0 || cam->h == 0 || (uint64_t)cam->w * cam->h > 0xFFFFFFFFull) return ZRT_ERR_INVALID_ARG;
     const uint32_t nranks = cfg->num_ranks ? cfg->num_ranks : 1;
     if (cfg->rank >= nranks) return ZRT_ERR_INVALID_ARG;
-    int maxb = 0;
     const bool want_stats = (cfg->flags & ZRT_FLAG_COUNT_STATS) != 0;
-    const TraceKernel tk = trace_fn(cfg->max_bounce, want_stats, c->v4_ok, &maxb);
-    if (!tk.fn) return ZRT_ERR_UNSUPPORTED;
-    TraceFn fn = tk.fn;
+    const bool want_prof = getenv("ZRT_PROFILE") != nullptr;
+    const TraceFn fn = trace_fn(cfg->max_bounce, want_stats, want_prof);
+    if (!fn) return ZRT_ERR_UNSUPPORTED;
     DeviceGuard g(c->device);
 
     // packed pixel order of this rank (cached across calls)
@@ -1049,10 +708,11 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     // occupancy-sized persistent grid
     int bpc = 0;
-    const size_t lds_bytes = 4ull * (tk.version == 4 ? c->occ4_words : c->occ_words);
+    const size_t lds_bytes = 4ull * c->occ_words;
     HIP_TRY(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)fn, tk.block, lds_bytes));
-    bpc = std::max(1, std::min(bpc, 8 * kBlock / tk.block));
+    const int tblock = trace_block();
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)fn, tblock, lds_bytes));
+    bpc = std::max(1, std::min(bpc, 2048 / tblock));
     const uint32_t grid_blocks = (uint32_t)(c->num_cus * bpc);
 
     TraceParams tp;
@@ -1078,17 +738,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.occ_nb0 = c->occ_nb[0];
     tp.occ_nb01 = c->occ_nb[0] * c->occ_nb[1];
     tp.occ_words = c->occ_words;
-    tp.occ4 = c->d_occ4;
-    tp.occ4_words = c->occ4_words;
-    tp.occ4_nbw = c->occ4_nbw;
-    tp.occ4_nb0 = c->occ4_nb[0];
-    tp.occ4_nb01 = c->occ4_nb[0] * c->occ4_nb[1];
     tp.w = cam->w;
     tp.pixlist = c->d_pix;
     tp.P = P;
     tp.max_bounce = cfg->max_bounce;
-    tp.chunk = std::max<uint32_t>(64, env_u32("ZRT_CHUNK", 512));
-    tp.shade_min = std::min<uint32_t>(64, std::max<uint32_t>(1, env_u32("ZRT_SHADE_MIN", 16)));
     tp.seed = cfg->seed;
     tp.out = c->d_out;
     tp.counter = c->d_counter;
@@ -1105,7 +758,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         tp.total = S * P;
         HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
         HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
-        hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tk.block), lds_bytes, c->stream, tp);
+        hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tblock), lds_bytes, c->stream, tp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
         hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,

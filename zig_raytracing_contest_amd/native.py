@@ -279,3 +279,49 @@ def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=N
     auxp = None if aux is None else np.ascontiguousarray(aux).ctypes.data
     check(lib().zrt_probe(which, inp.ctypes.data, out.ctypes.data, n, auxp, device), "zrt_probe")
     return out
+
+
+class Gltf:
+    """stage1: glTF/GLB load through the C ABI (zrt_gltf_*)."""
+
+    def __init__(self, path: str, num_threads: int = 0):
+        h = C.c_void_p()
+        check(lib().zrt_gltf_load(path.encode(), num_threads, C.byref(h)), f"zrt_gltf_load({path})")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.zrt_gltf_free(self._h)
+            self._h = None
+
+    def soup(self):
+        ptrs = [C.c_void_p() for _ in range(4)]
+        n = C.c_uint32(0)
+        check(lib().zrt_gltf_soup(self._h, *[C.byref(p) for p in ptrs], C.byref(n)), "zrt_gltf_soup")
+        k = n.value
+
+        def arr(p, shape, ctype, dtype):
+            if k == 0:
+                return np.zeros(shape, dtype)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ctype)), shape).copy()
+        return (arr(ptrs[0], (k, 9), C.c_float, np.float32), arr(ptrs[1], (k, 9), C.c_float, np.float32),
+                arr(ptrs[2], (k, 6), C.c_float, np.float32), arr(ptrs[3], (k,), C.c_uint32, np.uint32))
+
+    def materials(self):
+        s = Scene()
+        check(lib().zrt_gltf_materials(self._h, C.byref(s)), "zrt_gltf_materials")
+        desc = np.zeros((s.num_materials, 3, 7), np.int64)
+        for i in range(s.num_materials):
+            m = s.materials[i]
+            for k, name in enumerate(("base_color", "emissive", "transparency")):
+                t = getattr(m, name)
+                desc[i, k] = (t.offset, t.w, t.h, t.u_min, t.u_max, t.v_min, t.v_max)
+        tex = np.ctypeslib.as_array(s.texels, (s.num_texel_floats,)).copy()
+        return desc, tex
+
+    def camera(self, name=None, width=None, height=None) -> Camera:
+        cam = Camera()
+        check(lib().zrt_gltf_camera(self._h, None if name is None else name.encode(),
+                                    -1 if width is None else width, -1 if height is None else height,
+                                    C.byref(cam)), "zrt_gltf_camera")
+        return cam

@@ -523,3 +523,106 @@ def get_scene(name: str) -> SceneSoup:
     if name not in _cache:
         _cache[name] = SCENES[name]()
     return _cache[name]
+
+
+# ------------------------------------------------------------------ glTF out
+def write_gltf(soup: SceneSoup, path: str) -> str:
+    """Write `soup` as .gltf + .bin (+ .png textures) next to `path`.
+
+    Identity node transforms (positions/texcoords load back bit-exact; normals
+    load back as normalize(n), the reference's loader step), u16 indices as
+    the reference requires (meshes split into primitives of <= 21845
+    triangles), one node per camera carrying its matrix."""
+    import json
+    import os
+
+    from . import pngio
+    base = os.path.splitext(path)[0]
+    name = os.path.basename(base)
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    blob = bytearray()
+    views, accessors, prims = [], [], []
+
+    def add_view(arr: np.ndarray, target=None):
+        nonlocal blob
+        while len(blob) % 4:
+            blob += b"\0"
+        off = len(blob)
+        b = np.ascontiguousarray(arr).tobytes()
+        blob += b
+        v = {"buffer": 0, "byteOffset": off, "byteLength": len(b)}
+        if target:
+            v["target"] = target
+        views.append(v)
+        return len(views) - 1
+
+    # primitives = runs of consecutive triangles with one material (<= 21845
+    # triangles for u16 indices), so the loaded soup keeps the source order
+    per = 21845
+    runs, start = [], 0
+    mat = np.asarray(soup.mat)
+    for i in range(1, len(mat) + 1):
+        if i == len(mat) or mat[i] != mat[start] or i - start == per:
+            runs.append((start, i))
+            start = i
+    for a0, a1 in runs:
+        pos = soup.pos[a0:a1].reshape(-1, 3).astype(F32)
+        nrm = soup.nrm[a0:a1].reshape(-1, 3).astype(F32)
+        uv = soup.uv[a0:a1].reshape(-1, 2).astype(F32)
+        idx = np.arange(len(pos), dtype=np.uint16)
+        a = len(accessors)
+        accessors.append({"bufferView": add_view(pos, 34962), "componentType": 5126,
+                          "count": len(pos), "type": "VEC3",
+                          "min": [float(x) for x in pos.min(0)],
+                          "max": [float(x) for x in pos.max(0)]})
+        accessors.append({"bufferView": add_view(nrm, 34962), "componentType": 5126,
+                          "count": len(nrm), "type": "VEC3"})
+        accessors.append({"bufferView": add_view(uv, 34962), "componentType": 5126,
+                          "count": len(uv), "type": "VEC2"})
+        accessors.append({"bufferView": add_view(idx, 34963), "componentType": 5123,
+                          "count": len(idx), "type": "SCALAR"})
+        prims.append({"attributes": {"POSITION": a, "NORMAL": a + 1, "TEXCOORD_0": a + 2},
+                      "indices": a + 3, "material": int(mat[a0]), "mode": 4})
+    f = lambda x: float(np.float32(x))  # noqa: E731  f32-exact decimal
+    images, textures, samplers = [], [], []
+    for i, t in enumerate(soup.textures):
+        fn = f"{name}_tex{i}.png"
+        pngio.write(os.path.join(d, fn), t.rgba if t.has_alpha else t.rgba[..., :3])
+        images.append({"uri": fn})
+        samplers.append({"wrapS": 33071 if t.wrap_s_clamp else 10497,
+                         "wrapT": 33071 if t.wrap_t_clamp else 10497})
+        textures.append({"source": i, "sampler": i})
+    mats = []
+    for m in soup.materials:
+        md = {"name": m.name, "pbrMetallicRoughness": {"baseColorFactor": [f(x) for x in m.base_color]},
+              "emissiveFactor": [f(x) for x in m.emissive], "alphaMode": m.alpha_mode}
+        if m.alpha_mode == "MASK":
+            md["alphaCutoff"] = f(m.alpha_cutoff)
+        if m.base_texture is not None:
+            md["pbrMetallicRoughness"]["baseColorTexture"] = {"index": m.base_texture}
+        if m.emissive_texture is not None:
+            md["emissiveTexture"] = {"index": m.emissive_texture}
+        mats.append(md)
+    cams, nodes = [], [{"name": "scene", "mesh": 0}]
+    for c in soup.cameras:
+        persp = {"yfov": f(c.yfov), "znear": 0.01, "zfar": 1000.0}
+        if c.aspect is not None:
+            persp["aspectRatio"] = f(c.aspect)
+        cams.append({"name": c.name, "type": "perspective", "perspective": persp})
+        nodes.append({"name": c.name, "camera": len(cams) - 1,
+                      "matrix": [f(x) for x in np.asarray(c.matrix, F32)]})
+    bin_name = f"{name}.bin"
+    with open(os.path.join(d, bin_name), "wb") as fh:
+        fh.write(bytes(blob))
+    doc = {"asset": {"version": "2.0", "generator": "zig_raytracing_contest_amd.scenes"},
+           "scene": 0, "scenes": [{"nodes": list(range(len(nodes)))}], "nodes": nodes,
+           "meshes": [{"name": soup.name, "primitives": prims}], "materials": mats,
+           "cameras": cams, "buffers": [{"uri": bin_name, "byteLength": len(blob)}],
+           "bufferViews": views, "accessors": accessors}
+    if images:
+        doc.update(images=images, textures=textures, samplers=samplers)
+    out = os.path.join(d, f"{name}.gltf")
+    with open(out, "w") as fh:
+        json.dump(doc, fh)
+    return out
