@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes  # noqa: E402
+from zig_raytracing_contest_amd import dist as zdist  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # algorithmic bytes: 8 B per visited Cell, 36 B per triangle
@@ -63,20 +64,22 @@ def cpu_baseline(soup, cfg, target_s):
     threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16,
                          len(os.sched_getaffinity(0))))
     npx = cam.w * cam.h
-    spp = 4
 
-    def run(stride):
+    def run(stride, spp):
         pixels = np.arange(0, npx, stride, dtype=np.uint32)
         t0 = time.perf_counter()
         _, _, ctr = osc.render_pixels(cam, spp, cfg["max_bounce"], pixels, orc.RNG_REF, 0, threads)
         return time.perf_counter() - t0, ctr, pixels.size
 
-    dt, ctr, n = run(4096)                      # calibration
-    rate = max(ctr[0], 1) / max(dt, 1e-3)
-    want = rate * target_s                      # segments in ~target_s
-    seg_per_px = max(float(ctr[0]) / n, 1.0)
-    stride = max(1, int(npx / max(want / seg_per_px, 1.0)))
-    dt, ctr, n = run(stride)
+    dt, ctr, n = run(4096, 4)                   # calibration: ~500 pixels x 4 spp
+    seg_rate = max(float(ctr[0]), 1.0) / max(dt, 1e-3)
+    seg_per_sample = max(float(ctr[0]) / (n * 4), 1.0)
+    want_samples = seg_rate * target_s / seg_per_sample
+    spp = 4
+    stride = max(1, int(npx * spp / max(want_samples, 1.0)))
+    if stride == 1:                             # whole frame: raise spp instead
+        spp = int(min(64, max(4, want_samples / npx)))
+    dt, ctr, n = run(stride, spp)
     return {"value": round(float(ctr[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
             "kind": "port",
             "sample": f"{n} pixels (every {stride}th of {cam.w}x{cam.h}) x {spp} spp, "
@@ -104,20 +107,17 @@ def main():
 
     torch = None
     dev_buf = None
-    gather_bufs = None
     if world > 1:
         import torch
-        maxP = max(native.tile_pixels(cam.w, cam.h, 64, r, world).size for r in range(world))
-        dev_buf = torch.zeros(maxP * 3, dtype=torch.uint8, device=f"cuda:{local}")
-        gather_bufs = [torch.zeros_like(dev_buf) for _ in range(world)] if rank == 0 else None
+        dev_buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8,
+                              device=f"cuda:{local}")
 
     def step(stats=False):
         ptr = dev_buf.data_ptr() if dev_buf is not None else None
         res = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world,
                                 stats=stats, device_ptr=ptr)
-        if world > 1:
-            torch.cuda.synchronize()
-            dist.gather(dev_buf, gather_bufs, dst=0)
+        if world > 1:   # RCCL gather of the packed RGB8 tiles to rank 0 (+ unpermute)
+            zdist.gather_image(dev_buf, cam.w, cam.h, rank, world, dist)
         return res["stats"]
 
     # untimed counting run: exact algorithmic work of one step (same RNG ->

@@ -405,18 +405,16 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restric
 
 using TraceFn = void (*)(const TraceParams);
 
+// Timed kernel: launch bound (512 threads, 6 waves/SIMD) -> 80 VGPRs; the
+// few spills land outside the DDA loop and 6 waves hide more memory latency
+// than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
+constexpr int kMinWaves = 6;
+
 template <int MAXB>
 TraceFn pick(bool stats, bool prof) {
     if (prof) return (TraceFn)trace_kernel<MAXB, false, true, kTriBatch, 1>;
     if (stats) return (TraceFn)trace_kernel<MAXB, true, false, kTriBatch, 1>;
-    if (MAXB == 4) {
-        const char* e = getenv("ZRT_MINW");
-        const int w = e ? atoi(e) : 0;
-        if (w == 3) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 3>;
-        if (w == 6) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 6>;
-        if (w == 8) return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 8>;
-    }
-    return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, 1>;
+    return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, kMinWaves>;
 }
 
 // Threads per trace block: a multiple of 64, at most the launch bound.
