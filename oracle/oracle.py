@@ -76,7 +76,7 @@ def lib():
     L.orc_env.argtypes = [_f32p, _f32p]
     L.orc_tex_sample.argtypes = [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.c_float, C.c_float, _f32p]
-    for name, p in (("orc_xoshiro_u64", _u64p), ("orc_xoshiro_f32", _f32p),
+    for name, p in (("orc_xoshiro_u64", _u64p), ("orc_splitmix_u64", _u64p), ("orc_xoshiro_f32", _f32p),
                     ("orc_xoshiro_norm", _f32p)):
         getattr(L, name).argtypes = [C.c_uint64, p, C.c_int]
     for name, p in (("orc_path_u64", _u64p), ("orc_path_f32", _f32p), ("orc_path_norm", _f32p)):
@@ -160,6 +160,12 @@ def tex_sample(data, chans, w, h, u_min, u_max, v_min, v_max, u, v):
 def xoshiro_u64(seed, n):
     out = np.zeros(n, np.uint64)
     lib().orc_xoshiro_u64(seed, out, n)
+    return out
+
+
+def splitmix_u64(seed, n):
+    out = np.zeros(n, np.uint64)
+    lib().orc_splitmix_u64(seed, out, n)
     return out
 
 

@@ -873,6 +873,10 @@ void orc_tex_sample(const float* data, int chans, int w, int h, int u_min, int u
                     int v_max, float u, float v, float* out) {
     tex_sample_raw(data, chans, w, h, u_min, u_max, v_min, v_max, u, v, out);
 }
+void orc_splitmix_u64(uint64_t seed, uint64_t* out, int n) {
+    uint64_t s = seed;
+    for (int i = 0; i < n; ++i) { s += GOLDEN; out[i] = mix64(s); }
+}
 void orc_xoshiro_u64(uint64_t seed, uint64_t* out, int n) {
     rng_t r; rng_init_ref(&r, seed);
     for (int i = 0; i < n; ++i) out[i] = rng_next(&r);

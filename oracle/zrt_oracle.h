@@ -112,6 +112,7 @@ void  orc_tex_sample(const float* data, int chans, int w, int h, int u_min, int 
                      int v_min, int v_max, float u, float v, float* out);
 /* RNG streams */
 void  orc_xoshiro_u64(uint64_t seed, uint64_t* out, int n);
+void  orc_splitmix_u64(uint64_t seed, uint64_t* out, int n);   /* SplitMix64.init(seed).next() x n */
 void  orc_path_u64(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t* out, int n);
 void  orc_path_f32(uint64_t seed, uint32_t pixel, uint32_t sample, float* out, int n);
 void  orc_path_norm(uint64_t seed, uint32_t pixel, uint32_t sample, float* out, int n);
