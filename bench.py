@@ -155,7 +155,11 @@ def main():
         avg_launch_s = kern_ms / 1e3 / max(launches, 1)
         alg_bytes = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] +
                      B_HIT * cst["hits"] + B_PIX * P)
-        per_launch = alg_bytes / max(cst["trace_launches"], 1)
+        # the counting run takes the megakernel (1 launch/pass); the timed run
+        # takes the wavefront path (max_bounce launches/pass): bytes per timed
+        # launch = the step's bytes / the step's timed launches, so
+        # achieved = sum(bytes) / sum(launch durations) over the step.
+        per_launch = alg_bytes / max(launches / a.steps, 1)
         achieved = per_launch / avg_launch_s / 1e9
         out = {
             "metric": "Mrays/sec + wall-clock to output.png on contest config.json scene",
@@ -174,7 +178,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": None,
-                         "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "kernel": os.environ.get("ZRT_MODE", "wf") == "mega" and "trace_kernel" or "wf_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "alg_bytes_per_launch": int(per_launch)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},

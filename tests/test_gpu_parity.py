@@ -183,16 +183,24 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
         tuple(int(x) for x in ctr[:4])
 
 
-def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch):
+@pytest.mark.parametrize("mode", ["wf", "mega"])
+def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
+    """Pass splits (sample ranges), rank splits (tile sets) and the two kernel
+    organisations (wavefront / megakernel) all give the same image."""
     soup = scenes.get_scene("cornell")
     cam = camera_for(soup, None, 96, 80)
     rs = gpu_scenes("cornell")
+    monkeypatch.setenv("ZRT_MODE", "mega")
     ref, _ = rs.render(cam, num_samples=6, max_bounce=4)
-    monkeypatch.setenv("ZRT_PASS_BYTES", str(16 * 96 * 80 * 2))   # 2 samples per pass
+    monkeypatch.setenv("ZRT_MODE", mode)
+    per_item = 16 if mode == "mega" else 96 + 16 + 32 * 4
+    monkeypatch.setenv("ZRT_PASS_BYTES", str(per_item * 96 * 80 * 2))   # 2 samples per pass
+    monkeypatch.setenv("ZRT_WF_BYTES", str(per_item * 96 * 80 * 2))
     multi, r2 = rs.render(cam, num_samples=6, max_bounce=4)
-    assert r2["stats"]["trace_launches"] == 3
+    assert r2["stats"]["trace_launches"] == (3 if mode == "mega" else 3 * 4)
     assert np.array_equal(ref, multi)
     monkeypatch.delenv("ZRT_PASS_BYTES")
+    monkeypatch.delenv("ZRT_WF_BYTES")
     img = np.zeros_like(ref)
     for r in range(3):
         rs.render(cam, img=img, num_samples=6, max_bounce=4, rank=r, num_ranks=3)

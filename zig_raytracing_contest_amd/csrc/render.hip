@@ -380,6 +380,192 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wavefront mode: one launch per bounce over a compacted queue of live paths.
+//
+// The megakernel above keeps a lane on one path from camera to sky, so a
+// wave lives as long as its longest path (most waves hold a 4-segment path
+// while the mean is ~1.9: about half the lanes idle at the path level).  Here
+// bounce k is its own launch over the paths still alive after bounce k-1:
+// every lane traces exactly one segment and shades it; a continuing path is
+// appended to the next queue (one returning atomic per wave, ballot + mbcnt
+// ranks), a finished one stores its terminal radiance (env / 0) and the mask
+// of bounce slots that scattered.  The per-bounce (emissive, albedo) pairs go
+// to HBM in [slot][item] planes and the resolve kernel folds them back to
+// front per sample, then sums the samples in order: the arithmetic of
+// traceRayRecursive and renderWorker, bit for bit.
+//
+// A queue record is 48 B: (o.xyz, item) (d.xyz, depth | slot << 16)
+// (rng lo, rng hi, mask, 0).
+struct WfParams {
+    TraceParams t;
+    const float4* q_in;
+    const uint32_t* n_in;     // live paths in q_in (written by the previous launch)
+    float4* q_out;
+    uint32_t* n_out;
+    uint32_t* fetch;          // work counter of this launch
+    float4* stk;              // [(slot*2 + {0:e,1:a}) * T + item]
+    float4* term;             // [item]: terminal L.xyz, scatter mask bits
+    uint32_t T;               // items in this pass
+};
+
+template <int TB, int MINW, bool PRIMARY>
+__global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
+    const TraceParams& p = w.t;
+    __shared__ double s_zig[514];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
+    __syncthreads();
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t n = PRIMARY ? p.total : *w.n_in;
+    uint32_t n_seg = 0, dummy = 0;
+    uint64_t prof_dummy[2];
+
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(w.fetch, 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= n) break;
+        const uint32_t i = base + lane;
+        bool cont = false;
+        float4 r0, r1;
+        uint32_t rlo = 0, rhi = 0, mask = 0;
+        if (i < n) {
+            uint32_t item, depth, slot;
+            Rng rng;
+            v3 o, d;
+            if (PRIMARY) {
+                // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35)
+                item = i;
+                const uint32_t s_local = item / p.P;
+                const uint32_t q = item - s_local * p.P;
+                const uint32_t pixel = p.pixlist[q];
+                const uint32_t py = pixel / p.w;
+                const uint32_t px = pixel - py * p.w;
+                rng.s = path_key(p.seed, pixel, p.s0 + s_local);
+                const float jx = rng_float(rng);
+                const float jy = rng_float(rng);
+                o = mk(p.org[0], p.org[1], p.org[2]);
+                d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
+                                      scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
+                                  scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
+                depth = p.max_bounce;
+                slot = 0;
+            } else {
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                o = mk(a.x, a.y, a.z);
+                item = __float_as_uint(a.w);
+                d = mk(b.x, b.y, b.z);
+                depth = __float_as_uint(b.w) & 0xFFFFu;
+                slot = __float_as_uint(b.w) >> 16;
+                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+                mask = __float_as_uint(c.z);
+            }
+            v3 L = mk(0, 0, 0);
+            if (depth != 0) {
+                ++n_seg;
+                float hu = 0.0f, hv = 0.0f;
+                uint32_t hidx = 0;
+                const float t = trace_ray<false, false, TB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy,
+                                                            prof_dummy);
+                if (t == kInf) {
+                    L = env_color(d);                               // stage3.zig:195-197
+                } else {
+                    const float4* tdp = p.tri_data + 4ull * hidx;  // stage3.zig:199-206
+                    const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
+                    const float w0 = 1.0f - hu - hv;
+                    const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
+                    const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
+                    const DevMat& m = p.mats[__float_as_uint(d3.w)];
+                    const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
+                    const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
+                    const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
+                    const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
+                                       scale(mk(d1.z, d1.w, d2.x), hv));
+                    const v3 no = add(o, scale(d, t + kFltEps));
+                    if (!(rng_float(rng) > transparency)) {         // stage3.zig:207, :214-219
+                        const float nx = (float)rng_norm64(rng, zx, zf);
+                        const float ny = (float)rng_norm64(rng, zx, zf);
+                        const float nz = (float)rng_norm64(rng, zx, zf);
+                        d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+                        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
+                        w.stk[(2ull * slot + 1) * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
+                        mask |= 1u << slot;
+                    }
+                    o = no;
+                    --depth;
+                    ++slot;
+                    cont = depth != 0;                              // depth 0: recursion returns 0
+                }
+            }
+            if (!cont) {
+                w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
+            } else {
+                r0 = make_float4(o.x, o.y, o.z, __uint_as_float(item));
+                r1 = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
+                rlo = (uint32_t)rng.s;
+                rhi = (uint32_t)(rng.s >> 32);
+            }
+        }
+        // append the wave's continuing paths to the next queue
+        const uint64_t bal = __ballot(cont);
+        if (bal) {
+            uint32_t ob = 0;
+            if (lane == 0) ob = atomicAdd(w.n_out, (uint32_t)__popcll(bal));
+            ob = __builtin_amdgcn_readfirstlane(ob);
+            if (cont) {
+                const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
+                w.q_out[3ull * pos] = r0;
+                w.q_out[3ull * pos + 1] = r1;
+                w.q_out[3ull * pos + 2] = make_float4(__uint_as_float(rlo), __uint_as_float(rhi),
+                                                      __uint_as_float(mask), 0.0f);
+            }
+        }
+    }
+    const unsigned long long s0 = wave_sum(n_seg);
+    if (lane == 0) atomicAdd(&p.stats[0], s0);
+}
+
+// Fold + ordered sample sum + toRGB for wavefront mode (stage3.zig:219,
+// :236-242): per sample, L = terminal radiance, then e + a*L for every slot
+// that scattered, from the last bounce back to the first.
+__global__ __launch_bounds__(kBlock) void wf_resolve_kernel(const float4* __restrict__ term,
+                                                            const float4* __restrict__ stk, uint32_t T,
+                                                            uint32_t P, uint32_t S, uint32_t max_bounce,
+                                                            float4* acc, int first, int last,
+                                                            float inv_spp, uint8_t* rgb, float* lin) {
+    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= P) return;
+    v3 px = mk(0, 0, 0);
+    if (!first) { const float4 a = acc[q]; px = mk(a.x, a.y, a.z); }
+    for (uint32_t s = 0; s < S; ++s) {
+        const uint32_t item = s * P + q;
+        const float4 tm = term[item];
+        v3 L = mk(tm.x, tm.y, tm.z);
+        const uint32_t mask = __float_as_uint(tm.w);
+        for (int slot = (int)max_bounce - 1; slot >= 0; --slot) {
+            if ((mask >> slot) & 1u) {
+                const float4 e = stk[(2ull * slot) * T + item];
+                const float4 a = stk[(2ull * slot + 1) * T + item];
+                L = add(mk(e.x, e.y, e.z), mul(mk(a.x, a.y, a.z), L));
+            }
+        }
+        px = add(px, L);
+    }
+    if (!last) { acc[q] = make_float4(px.x, px.y, px.z, 0.0f); return; }
+    const v3 l = mul(px, mk(inv_spp, inv_spp, inv_spp));
+    uint8_t c[3];
+    to_rgb(l, c);
+    rgb[3 * (size_t)q + 0] = c[0];
+    rgb[3 * (size_t)q + 1] = c[1];
+    rgb[3 * (size_t)q + 2] = c[2];
+    if (lin) { lin[3 * (size_t)q] = l.x; lin[3 * (size_t)q + 1] = l.y; lin[3 * (size_t)q + 2] = l.z; }
+}
+
 // renderWorker tail (stage3.zig:236-242): ordered per-pixel sum over this
 // pass's samples, then (last pass) * (1/spp) and toRGB.
 __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restrict__ out, uint32_t P,
@@ -409,6 +595,7 @@ using TraceFn = void (*)(const TraceParams);
 // few spills land outside the DDA loop and 6 waves hide more memory latency
 // than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
 constexpr int kMinWaves = 6;
+constexpr int kWfMinWaves = 6;
 
 template <int MAXB>
 TraceFn pick(bool stats, bool prof) {
@@ -477,6 +664,11 @@ struct zrt_context {
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;
+    float4* d_q0 = nullptr; size_t q0_cap = 0;       // wavefront queues
+    float4* d_q1 = nullptr; size_t q1_cap = 0;
+    float4* d_term = nullptr; size_t term_cap = 0;
+    float4* d_stk = nullptr; size_t stk_cap = 0;
+    uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
     float* d_lin = nullptr; size_t lin_cap = 0;
@@ -529,7 +721,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
-                    c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
+                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -649,6 +841,12 @@ extern "C" int zrt_context_create(const zrt_scene* s, int device, zrt_context** 
     return ZRT_OK;
 }
 
+static size_t wf_budget_bytes() {
+    const char* e = getenv("ZRT_WF_BYTES");
+    if (e) { const long long v = atoll(e); if (v > 0) return (size_t)v; }
+    return (size_t)40 << 30;   // queues + bounce stack of one pass (HBM is 288 GB)
+}
+
 static size_t pass_budget_bytes() {
     const char* e = getenv("ZRT_PASS_BYTES");
     if (e) { const long long v = atoll(e); if (v > 0) return (size_t)v; }
@@ -688,12 +886,34 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (P == 0) { if (stats) *stats = st; return ZRT_OK; }
 
     const uint32_t spp = cfg->num_samples;
-    uint64_t s_pass = std::max<uint64_t>(1, pass_budget_bytes() / (16ull * P));
+    const uint32_t mb = cfg->max_bounce;
+    // wavefront (default) or megakernel; the counting variant is a megakernel
+    const char* mode_env = getenv("ZRT_MODE");
+    const bool wf = !want_stats && !want_prof && !(mode_env && strcmp(mode_env, "mega") == 0);
+    // per-item bytes of a pass: megakernel = the float4 sample radiance;
+    // wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per bounce slot
+    const uint64_t per_item = wf ? (96ull + 16ull + 32ull * std::max<uint32_t>(mb, 1)) : 16ull;
+    size_t budget = wf ? wf_budget_bytes() : pass_budget_bytes();
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+            budget = std::min(budget, free_b / 10 * 6);
+    }
+    uint64_t s_pass = std::max<uint64_t>(1, budget / (per_item * P));
     s_pass = std::min<uint64_t>(s_pass, spp);
     s_pass = std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
-    int rc = grow(&c->d_out, &c->out_cap, (size_t)s_pass * P);
-    if (rc != ZRT_OK) return rc;
+    const uint64_t T = s_pass * P;
+    int rc;
+    if (wf) {
+        if ((rc = grow(&c->d_q0, &c->q0_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * std::max<uint32_t>(mb, 1))) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 2ull * (mb + 2))) != ZRT_OK) return rc;
+    } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
+        return rc;
+    }
     if (npasses > 1 && (rc = grow(&c->d_acc, &c->acc_cap, P)) != ZRT_OK) return rc;
     if ((rc = grow(&c->d_rgb, &c->rgb_cap, 3ull * P)) != ZRT_OK) return rc;
     const bool want_lin = outs && outs->linear_packed;
@@ -704,14 +924,33 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         c->ev_trace.push_back(e);
     }
 
-    // occupancy-sized persistent grid
-    int bpc = 0;
+    // occupancy-sized persistent grids
     const size_t lds_bytes = 4ull * c->occ_words;
-    HIP_TRY(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
     const int tblock = trace_block();
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void*)fn, tblock, lds_bytes));
-    bpc = std::max(1, std::min(bpc, 2048 / tblock));
-    const uint32_t grid_blocks = (uint32_t)(c->num_cus * bpc);
+    auto grid_for = [&](const void* f, uint32_t* blocks) -> int {
+        int bpc = 0;
+        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, f, tblock, lds_bytes));
+        bpc = std::max(1, std::min(bpc, 2048 / tblock));
+        *blocks = (uint32_t)(c->num_cus * bpc);
+        return ZRT_OK;
+    };
+    using WfFn = void (*)(const WfParams);
+    WfFn wf_first = (WfFn)wf_kernel<kTriBatch, kWfMinWaves, true>;
+    WfFn wf_next = (WfFn)wf_kernel<kTriBatch, kWfMinWaves, false>;
+    if (const char* e = getenv("ZRT_WF_MINW")) {   // tuning sweep only
+        const int w = atoi(e);
+        if (w == 4) { wf_first = (WfFn)wf_kernel<kTriBatch, 4, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 4, false>; }
+        if (w == 5) { wf_first = (WfFn)wf_kernel<kTriBatch, 5, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 5, false>; }
+        if (w == 8) { wf_first = (WfFn)wf_kernel<kTriBatch, 8, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 8, false>; }
+    }
+    uint32_t grid_blocks = 0, grid_first = 0, grid_next = 0;
+    if (wf) {
+        if ((rc = grid_for((const void*)wf_first, &grid_first)) != ZRT_OK) return rc;
+        if ((rc = grid_for((const void*)wf_next, &grid_next)) != ZRT_OK) return rc;
+    } else if ((rc = grid_for((const void*)fn, &grid_blocks)) != ZRT_OK) {
+        return rc;
+    }
 
     TraceParams tp;
     memset(&tp, 0, sizeof tp);
@@ -739,7 +978,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.w = cam->w;
     tp.pixlist = c->d_pix;
     tp.P = P;
-    tp.max_bounce = cfg->max_bounce;
+    tp.max_bounce = mb;
     tp.seed = cfg->seed;
     tp.out = c->d_out;
     tp.counter = c->d_counter;
@@ -749,19 +988,53 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
+    uint32_t launches = 0;
     for (uint32_t pass = 0; pass < npasses; ++pass) {
         const uint32_t s0 = (uint32_t)(pass * s_pass);
         const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
         tp.s0 = s0;
         tp.total = S * P;
-        HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
-        HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
-        hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tblock), lds_bytes, c->stream, tp);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
-        hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
-                           c->d_out, P, S, c->d_acc, pass == 0 ? 1 : 0, pass + 1 == npasses ? 1 : 0,
-                           inv_spp, c->d_rgb, want_lin ? c->d_lin : nullptr);
+        const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
+        if (wf) {
+            // counters: n[k] = live paths entering bounce k, fetch[k] = work counter of launch k
+            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 8ull * (mb + 2), c->stream));
+            uint32_t* n = c->d_wfc;
+            uint32_t* fetch = c->d_wfc + (mb + 2);
+            WfParams W;
+            W.t = tp;
+            W.stk = c->d_stk;
+            W.term = c->d_term;
+            W.T = (uint32_t)T;
+            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
+            const uint32_t nb = std::max<uint32_t>(mb, 1);
+            for (uint32_t k = 0; k < nb; ++k) {
+                W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
+                W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
+                W.n_in = n + k;
+                W.n_out = n + k + 1;
+                W.fetch = fetch + k;
+                if (k == 0)
+                    hipLaunchKernelGGL(wf_first, dim3(grid_first), dim3(tblock), lds_bytes, c->stream, W);
+                else
+                    hipLaunchKernelGGL(wf_next, dim3(grid_next), dim3(tblock), lds_bytes, c->stream, W);
+                HIP_TRY(hipGetLastError());
+                ++launches;
+            }
+            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
+            hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                               c->d_term, c->d_stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
+                               c->d_rgb, want_lin ? c->d_lin : nullptr);
+        } else {
+            HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
+            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
+            hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tblock), lds_bytes, c->stream, tp);
+            HIP_TRY(hipGetLastError());
+            ++launches;
+            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
+            hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                               c->d_out, P, S, c->d_acc, first, last, inv_spp, c->d_rgb,
+                               want_lin ? c->d_lin : nullptr);
+        }
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev_end, c->stream));
@@ -784,7 +1057,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[2 * pass], c->ev_trace[2 * pass + 1]));
         st.trace_kernel_ms += t;
     }
-    st.trace_launches = npasses;
+    st.trace_launches = launches;
     st.segments = hs[0];
     st.cells_visited = hs[1];
     st.triangle_tests = hs[2];
