@@ -183,17 +183,22 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
         tuple(int(x) for x in ctr[:4])
 
 
-@pytest.mark.parametrize("mode", ["wf", "mega"])
+# per-item pass bytes of each kernel organisation (render.hip: per_item)
+PER_ITEM = {"mega": 16, "wf": 96 + 16 + 32 * 4, "split": 96 + 16 + 16 + 32 * 4}
+
+
+@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
 def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
-    """Pass splits (sample ranges), rank splits (tile sets) and the two kernel
-    organisations (wavefront / megakernel) all give the same image."""
+    """Pass splits (sample ranges), rank splits (tile sets) and the three kernel
+    organisations (fused wavefront / split wavefront / megakernel) all give the
+    same image."""
     soup = scenes.get_scene("cornell")
     cam = camera_for(soup, None, 96, 80)
     rs = gpu_scenes("cornell")
     monkeypatch.setenv("ZRT_MODE", "mega")
     ref, _ = rs.render(cam, num_samples=6, max_bounce=4)
     monkeypatch.setenv("ZRT_MODE", mode)
-    per_item = 16 if mode == "mega" else 96 + 16 + 32 * 4
+    per_item = PER_ITEM[mode]
     monkeypatch.setenv("ZRT_PASS_BYTES", str(per_item * 96 * 80 * 2))   # 2 samples per pass
     monkeypatch.setenv("ZRT_WF_BYTES", str(per_item * 96 * 80 * 2))
     multi, r2 = rs.render(cam, num_samples=6, max_bounce=4)
@@ -207,8 +212,10 @@ def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
     assert np.array_equal(ref, img)
 
 
+@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
 @pytest.mark.parametrize("mb", [0, 1, 5, 9, 17])
-def test_render_max_bounce_variants(oracle_mod, gpu_scenes, mb):
+def test_render_max_bounce_variants(oracle_mod, gpu_scenes, monkeypatch, mode, mb):
+    monkeypatch.setenv("ZRT_MODE", mode)
     soup = scenes.get_scene("cornell")
     c = soup.camera()
     cam = camera_for(soup, None, 40, 40)

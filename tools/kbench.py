@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg3")
 ap.add_argument("--spp", type=int, default=64)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--cell-stats", action="store_true", help="one counting render first (ZRT_CELL_STATS)")
 ap.add_argument("--var", action="append", default=[], help="ENV=VAL[,ENV=VAL] per variant")
 a = ap.parse_args()
 cfg = scenes.CONFIGS[a.config]
@@ -25,6 +26,12 @@ geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
 keep = []
 native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
 ref = None
+if a.cell_stats:
+    os.environ["ZRT_CELL_STATS"] = "1"
+    ctx = native.Context(geo.scene)
+    r = ctx.render(cam, a.spp, cfg["max_bounce"], stats=True)
+    print(json.dumps({"stats": {k: v for k, v in r["stats"].items()}}), flush=True)
+    ctx.close()
 for var in (a.var or [""]):
     env = dict(kv.split("=") for kv in var.split(",") if kv)
     old = {k: os.environ.get(k) for k in env}

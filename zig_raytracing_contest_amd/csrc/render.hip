@@ -156,8 +156,24 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
 // (nearest <= inf).  CROSSED: the step left the current occupancy brick.
 // A macro over a local Dda, not a function on a reference: as a function,
 // InstCombine turns `a0 ? s.c0 : s.c1` into a load through a selected
-// pointer and the whole state lands in scratch memory.
-#define DDA_STEP(S, P, SH, CROSSED, T_EXIT)                                           \
+// pointer and the whole state lands in scratch memory.  For the same reason
+// the grid constants come in as a GridK of laundered registers: selecting
+// between p.res[0..2] directly became a global load from the kernel
+// arguments at a selected offset, i.e. a memory round trip in every step.
+struct GridK {
+    uint32_t rm0, rm1, rm2;   // res[k] - 1: last cell index per axis
+    uint32_t str1, str2;      // linear-index strides of axes 1 and 2
+};
+__device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
+    GridK g;
+    g.rm0 = __builtin_amdgcn_readfirstlane(p.res[0] - 1u);
+    g.rm1 = __builtin_amdgcn_readfirstlane(p.res[1] - 1u);
+    g.rm2 = __builtin_amdgcn_readfirstlane(p.res[2] - 1u);
+    g.str1 = __builtin_amdgcn_readfirstlane(p.res[0]);
+    g.str2 = __builtin_amdgcn_readfirstlane(p.res[0] * p.res[1]);
+    return g;
+}
+#define DDA_STEP(S, G, SH, CROSSED, T_EXIT)                                           \
     do {                                                                             \
         const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
         const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
@@ -169,10 +185,10 @@ __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda&
         const uint32_t cc_ = a0_ ? c0_ : (a1_ ? c1_ : c2_);                          \
         const uint32_t ax_ = a0_ ? 0u : (a1_ ? 1u : 2u);                             \
         const bool ng_ = ((S).neg >> ax_) & 1u;                                      \
-        const uint32_t rm1_ = (a0_ ? (P).res[0] : (a1_ ? (P).res[1] : (P).res[2])) - 1u; \
+        const uint32_t rm1_ = a0_ ? (G).rm0 : (a1_ ? (G).rm1 : (G).rm2);           \
         const uint32_t ec_ = ng_ ? 0u : rm1_;                                        \
         const uint32_t cn_ = ng_ ? cc_ - 1u : cc_ + 1u;                              \
-        const uint32_t str_ = a0_ ? 1u : (a1_ ? (P).res[0] : (P).res[0] * (P).res[1]); \
+        const uint32_t str_ = a0_ ? 1u : (a1_ ? (G).str1 : (G).str2);             \
         (CROSSED) = ((cc_ ^ cn_) >> (SH)) != 0u;                                     \
         const float u0_ = t0_ + (S).td0, u1_ = t1_ + (S).td1, u2_ = t2_ + (S).td2;   \
         (S).tn0 = a0_ ? u0_ : t0_;                                                   \
@@ -235,6 +251,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
     Dda s;
     if (!dda_setup(p, o, d, s)) return nearest;
     const uint32_t sh = p.occ_shift;
+    const GridK gk = grid_consts(p);
     bool occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
     for (;;) {
         uint64_t ta = 0, tb = 0;
@@ -242,12 +259,13 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         if (STATS) ++n_cells;
         if (occupied) {
             const uint2 cell = p.cells[s.lin];
+            if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; }
             test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests);
         }
         if (PROF) tb = stamp();
         bool crossed;
         float t_exit;
-        DDA_STEP(s, p, sh, crossed, t_exit);
+        DDA_STEP(s, gk, sh, crossed, t_exit);
         if (nearest <= t_exit) break;                      // stage3.zig:179-182
         if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
         if (PROF) { const uint64_t tc = stamp(); prof[0] += tb - ta; prof[1] += tc - tb; }
@@ -286,7 +304,8 @@ template <int MAXB, bool STATS, bool PROF, int TB, int MINW>
 __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TraceParams p) {
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    uint64_t prof[6] = {0, 0, 0, 0, 0, 0};   // cell+tris, dda, trace, shade, fetch, total
+    // cell+tris, dda, trace, shade, fetch, total (PROF); cell loads, non-empty cells (STATS)
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_begin = PROF ? stamp() : 0;
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
@@ -369,13 +388,19 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     }
     const unsigned long long s0 = wave_sum(n_seg);
     unsigned long long s1 = 0, s2 = 0, s3 = 0;
-    if (STATS) { s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits); }
+    unsigned long long s4 = 0, s5 = 0;
+    if (STATS) {
+        s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits);
+        s4 = wave_sum(prof[6]); s5 = wave_sum(prof[7]);
+    }
     if (lane == 0) {
         atomicAdd(&p.stats[0], s0);
         if (STATS) {
             atomicAdd(&p.stats[1], s1);
             atomicAdd(&p.stats[2], s2);
             atomicAdd(&p.stats[3], s3);
+            atomicAdd(&p.stats[4], s4);
+            atomicAdd(&p.stats[5], s5);
         }
     }
 }
@@ -406,8 +431,86 @@ struct WfParams {
     uint32_t* fetch;          // work counter of this launch
     float4* stk;              // [(slot*2 + {0:e,1:a}) * T + item]
     float4* term;             // [item]: terminal L.xyz, scatter mask bits
+    float4* hit;              // split mode: [queue index] (t, u, v, tri) of this bounce
     uint32_t T;               // items in this pass
+    uint32_t refill;          // split mode: idle lanes before a wave fetches rays
 };
+
+// renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35) for
+// pass item `item` (= s_local * P + packed pixel); leaves rng after the jitter.
+__device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, Rng& rng, v3& o, v3& d) {
+    const uint32_t s_local = item / p.P;
+    const uint32_t q = item - s_local * p.P;
+    const uint32_t pixel = p.pixlist[q];
+    const uint32_t py = pixel / p.w;
+    const uint32_t px = pixel - py * p.w;
+    rng.s = path_key(p.seed, pixel, p.s0 + s_local);
+    const float jx = rng_float(rng);
+    const float jy = rng_float(rng);
+    o = mk(p.org[0], p.org[1], p.org[2]);
+    d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
+                          scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
+                      scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
+}
+
+// traceRayRecursive's body after the hit (stage3.zig:195-219) for one
+// segment: env colour on a miss, else material lookup, (e, a) pair to the
+// bounce stack on a scatter, pass-through otherwise.  Returns true when the
+// path continues (o, d, depth, slot, rng, mask updated); false with L set
+// when it terminates.
+__device__ __forceinline__ bool shade_segment(const WfParams& w, const double* zx, const double* zf,
+                                              uint32_t item, float t, float hu, float hv, uint32_t hidx,
+                                              v3& o, v3& d, uint32_t& depth, uint32_t& slot, Rng& rng,
+                                              uint32_t& mask, v3& L) {
+    const TraceParams& p = w.t;
+    if (t == kInf) { L = env_color(d); return false; }     // stage3.zig:195-197
+    const float4* tdp = p.tri_data + 4ull * hidx;          // stage3.zig:199-206
+    const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
+    const float w0 = 1.0f - hu - hv;
+    const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
+    const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
+    const DevMat& m = p.mats[__float_as_uint(d3.w)];
+    const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
+    const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
+    const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
+    const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
+                       scale(mk(d1.z, d1.w, d2.x), hv));
+    const v3 no = add(o, scale(d, t + kFltEps));
+    if (!(rng_float(rng) > transparency)) {                 // stage3.zig:207, :214-219
+        const float nx = (float)rng_norm64(rng, zx, zf);
+        const float ny = (float)rng_norm64(rng, zx, zf);
+        const float nz = (float)rng_norm64(rng, zx, zf);
+        d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
+        w.stk[(2ull * slot + 1) * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
+        mask |= 1u << slot;
+    }
+    o = no;
+    --depth;
+    ++slot;
+    L = mk(0, 0, 0);
+    return depth != 0;                                      // depth 0: recursion returns 0
+}
+
+// Append the wave's continuing paths to the next queue: one returning atomic
+// per wave, ranks from ballot + popcount.
+__device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d,
+                                         uint32_t item, uint32_t depth, uint32_t slot, const Rng& rng,
+                                         uint32_t mask) {
+    const uint64_t bal = __ballot(cont);
+    if (!bal) return;
+    uint32_t ob = 0;
+    if ((threadIdx.x & 63u) == 0) ob = atomicAdd(w.n_out, (uint32_t)__popcll(bal));
+    ob = __builtin_amdgcn_readfirstlane(ob);
+    if (cont) {
+        const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
+        w.q_out[3ull * pos] = make_float4(o.x, o.y, o.z, __uint_as_float(item));
+        w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
+        w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s),
+                                              __uint_as_float((uint32_t)(rng.s >> 32)),
+                                              __uint_as_float(mask), 0.0f);
+    }
+}
 
 template <int TB, int MINW, bool PRIMARY>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
@@ -432,27 +535,17 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
         if (base >= n) break;
         const uint32_t i = base + lane;
         bool cont = false;
-        float4 r0, r1;
-        uint32_t rlo = 0, rhi = 0, mask = 0;
+        uint32_t mask = 0, r_item = 0, r_depth = 0, r_slot = 0;
+        v3 r_o = mk(0, 0, 0), r_d = mk(0, 0, 0);
+        Rng r_rng;
+        r_rng.s = 0;
         if (i < n) {
             uint32_t item, depth, slot;
             Rng rng;
             v3 o, d;
             if (PRIMARY) {
-                // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35)
                 item = i;
-                const uint32_t s_local = item / p.P;
-                const uint32_t q = item - s_local * p.P;
-                const uint32_t pixel = p.pixlist[q];
-                const uint32_t py = pixel / p.w;
-                const uint32_t px = pixel - py * p.w;
-                rng.s = path_key(p.seed, pixel, p.s0 + s_local);
-                const float jx = rng_float(rng);
-                const float jy = rng_float(rng);
-                o = mk(p.org[0], p.org[1], p.org[2]);
-                d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
-                                      scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
-                                  scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
+                camera_ray(p, item, rng, o, d);
                 depth = p.max_bounce;
                 slot = 0;
             } else {
@@ -472,59 +565,150 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
                 uint32_t hidx = 0;
                 const float t = trace_ray<false, false, TB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy,
                                                             prof_dummy);
-                if (t == kInf) {
-                    L = env_color(d);                               // stage3.zig:195-197
-                } else {
-                    const float4* tdp = p.tri_data + 4ull * hidx;  // stage3.zig:199-206
-                    const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
-                    const float w0 = 1.0f - hu - hv;
-                    const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
-                    const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
-                    const DevMat& m = p.mats[__float_as_uint(d3.w)];
-                    const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
-                    const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
-                    const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
-                    const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
-                                       scale(mk(d1.z, d1.w, d2.x), hv));
-                    const v3 no = add(o, scale(d, t + kFltEps));
-                    if (!(rng_float(rng) > transparency)) {         // stage3.zig:207, :214-219
-                        const float nx = (float)rng_norm64(rng, zx, zf);
-                        const float ny = (float)rng_norm64(rng, zx, zf);
-                        const float nz = (float)rng_norm64(rng, zx, zf);
-                        d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
-                        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
-                        w.stk[(2ull * slot + 1) * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
-                        mask |= 1u << slot;
+                cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
+            }
+            if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
+            r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
+        }
+        wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask);
+    }
+    const unsigned long long s0 = wave_sum(n_seg);
+    if (lane == 0) atomicAdd(&p.stats[0], s0);
+}
+
+// Split wavefront (default): bounce k = wf_trace_kernel (Scene.traceRay only)
+// + wf_shade_kernel (the rest of the segment, one lane per path).
+//
+// Traversal lengths within a wave differ by 10x or more (a ray grazing the
+// ground plane crosses 200 cells, one hitting the object next to it 3), so
+// a wave that traces 64 rays start to finish idles most lanes most of the
+// time.  Here the unit of work in the loop is ONE grid cell: a lane whose ray
+// has finished writes its hit record and goes idle, and once `refill` lanes
+// of the wave are idle they fetch fresh rays from the queue together (one
+// atomic per wave) while the others keep walking (persistent threads with
+// dynamic ray fetch).  The per-ray state is only the ray, the DDA state and
+// the best hit; shading lives in its own kernel so none of its registers
+// are live in the traversal loop.
+template <int TB, int MINW, bool PRIMARY>
+__global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfParams w) {
+    const TraceParams& p = w.t;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
+    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t n = PRIMARY ? p.total : *w.n_in;
+    const uint32_t refill = w.refill;
+    const uint32_t sh = p.occ_shift;
+    const GridK gk = grid_consts(p);
+    bool active = false, occupied = false, more = n != 0;
+    uint32_t ray = 0, hidx = 0;
+    float nearest = kInf, hu = 0.0f, hv = 0.0f;
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+    Dda s;
+    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
+    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (more && nidle >= refill) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(w.fetch, nidle);
+            base = __builtin_amdgcn_readfirstlane(base);
+            more = base < n && n - base > nidle;
+            if (!active) {
+                const uint32_t r = base + (uint32_t)__popcll(idle & below);
+                if (base < n && r < n) {
+                    ray = r;
+                    if (PRIMARY) {
+                        Rng rng;
+                        camera_ray(p, r, rng, o, d);
+                    } else {
+                        const float4 a = w.q_in[3ull * r], b = w.q_in[3ull * r + 1];
+                        o = mk(a.x, a.y, a.z);
+                        d = mk(b.x, b.y, b.z);
                     }
-                    o = no;
-                    --depth;
-                    ++slot;
-                    cont = depth != 0;                              // depth 0: recursion returns 0
+                    nearest = kInf;
+                    hu = hv = 0.0f;
+                    hidx = 0;
+                    if (dda_setup(p, o, d, s)) {                   // stage3.zig:153-156
+                        active = true;
+                        occupied = brick_occupied(p, s_occ, s.c0, s.c1, s.c2);
+                    } else {
+                        w.hit[r] = make_float4(kInf, 0.0f, 0.0f, 0.0f);
+                    }
                 }
             }
-            if (!cont) {
-                w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
+        }
+        if (__ballot(active) == 0) {
+            if (!more) break;
+            continue;
+        }
+        if (active) {
+            if (occupied) {
+                const uint2 cell = p.cells[s.lin];
+                uint32_t nt = 0;
+                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, nt);
+            }
+            bool crossed;
+            float t_exit;
+            DDA_STEP(s, gk, sh, crossed, t_exit);
+            if (nearest <= t_exit) {                               // stage3.zig:179-182
+                w.hit[ray] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
+                active = false;
+            } else if (crossed) {
+                occupied = brick_occupied(p, s_occ, s.c0, s.c1, s.c2);
+            }
+        }
+    }
+}
+
+template <bool PRIMARY>
+__global__ __launch_bounds__(kBlock) void wf_shade_kernel(const WfParams w) {
+    const TraceParams& p = w.t;
+    __shared__ double s_zig[514];
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    __syncthreads();
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t n = PRIMARY ? p.total : *w.n_in;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint32_t n_seg = 0;
+    for (uint32_t base = wave * 64u; base < n; base += nwaves * 64u) {
+        const uint32_t i = base + lane;
+        bool cont = false;
+        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
+        Rng rng;
+        rng.s = 0;
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (i < n) {
+            if (PRIMARY) {
+                item = i;
+                camera_ray(p, item, rng, o, d);
+                depth = p.max_bounce;
             } else {
-                r0 = make_float4(o.x, o.y, o.z, __uint_as_float(item));
-                r1 = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
-                rlo = (uint32_t)rng.s;
-                rhi = (uint32_t)(rng.s >> 32);
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                o = mk(a.x, a.y, a.z);
+                item = __float_as_uint(a.w);
+                d = mk(b.x, b.y, b.z);
+                depth = __float_as_uint(b.w) & 0xFFFFu;
+                slot = __float_as_uint(b.w) >> 16;
+                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+                mask = __float_as_uint(c.z);
             }
-        }
-        // append the wave's continuing paths to the next queue
-        const uint64_t bal = __ballot(cont);
-        if (bal) {
-            uint32_t ob = 0;
-            if (lane == 0) ob = atomicAdd(w.n_out, (uint32_t)__popcll(bal));
-            ob = __builtin_amdgcn_readfirstlane(ob);
-            if (cont) {
-                const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
-                w.q_out[3ull * pos] = r0;
-                w.q_out[3ull * pos + 1] = r1;
-                w.q_out[3ull * pos + 2] = make_float4(__uint_as_float(rlo), __uint_as_float(rhi),
-                                                      __uint_as_float(mask), 0.0f);
+            v3 L = mk(0, 0, 0);
+            if (depth != 0) {               // max_bounce 0: black, nothing traced
+                ++n_seg;
+                const float4 h = w.hit[i];
+                cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth,
+                                     slot, rng, mask, L);
             }
+            if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
         }
+        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -596,6 +780,7 @@ using TraceFn = void (*)(const TraceParams);
 // than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
 constexpr int kMinWaves = 6;
 constexpr int kWfMinWaves = 6;
+constexpr int kSplitMinWaves = 6;
 
 template <int MAXB>
 TraceFn pick(bool stats, bool prof) {
@@ -668,6 +853,7 @@ struct zrt_context {
     float4* d_q1 = nullptr; size_t q1_cap = 0;
     float4* d_term = nullptr; size_t term_cap = 0;
     float4* d_stk = nullptr; size_t stk_cap = 0;
+    float4* d_hit = nullptr; size_t hit_cap = 0;
     uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
@@ -721,7 +907,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
-                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
+                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_hit, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -890,9 +1076,14 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // wavefront (default) or megakernel; the counting variant is a megakernel
     const char* mode_env = getenv("ZRT_MODE");
     const bool wf = !want_stats && !want_prof && !(mode_env && strcmp(mode_env, "mega") == 0);
+    // "wf" (default): one fused trace+shade kernel per bounce; "split":
+    // wf_trace_kernel (lane refill) + wf_shade_kernel per bounce
+    const bool split = wf && mode_env && strcmp(mode_env, "split") == 0;
     // per-item bytes of a pass: megakernel = the float4 sample radiance;
-    // wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per bounce slot
-    const uint64_t per_item = wf ? (96ull + 16ull + 32ull * std::max<uint32_t>(mb, 1)) : 16ull;
+    // wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per bounce
+    // slot (+ the 16 B hit record in split mode)
+    const uint64_t per_item = wf ? (96ull + 16ull + (split ? 16ull : 0ull) + 32ull * std::max<uint32_t>(mb, 1))
+                                 : 16ull;
     size_t budget = wf ? wf_budget_bytes() : pass_budget_bytes();
     {
         size_t free_b = 0, total_b = 0;
@@ -911,6 +1102,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * std::max<uint32_t>(mb, 1))) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_wfc, &c->wfc_cap, 2ull * (mb + 2))) != ZRT_OK) return rc;
+        if (split && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
     }
@@ -918,7 +1110,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if ((rc = grow(&c->d_rgb, &c->rgb_cap, 3ull * P)) != ZRT_OK) return rc;
     const bool want_lin = outs && outs->linear_packed;
     if (want_lin && (rc = grow(&c->d_lin, &c->lin_cap, 3ull * P)) != ZRT_OK) return rc;
-    while (c->ev_trace.size() < 2ull * npasses) {
+    const uint32_t launches_per_pass = wf ? std::max<uint32_t>(mb, 1) : 1;
+    while (c->ev_trace.size() < 2ull * npasses * launches_per_pass) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
         c->ev_trace.push_back(e);
@@ -936,13 +1129,26 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         return ZRT_OK;
     };
     using WfFn = void (*)(const WfParams);
-    WfFn wf_first = (WfFn)wf_kernel<kTriBatch, kWfMinWaves, true>;
-    WfFn wf_next = (WfFn)wf_kernel<kTriBatch, kWfMinWaves, false>;
-    if (const char* e = getenv("ZRT_WF_MINW")) {   // tuning sweep only
-        const int w = atoi(e);
-        if (w == 4) { wf_first = (WfFn)wf_kernel<kTriBatch, 4, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 4, false>; }
-        if (w == 5) { wf_first = (WfFn)wf_kernel<kTriBatch, 5, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 5, false>; }
-        if (w == 8) { wf_first = (WfFn)wf_kernel<kTriBatch, 8, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 8, false>; }
+    WfFn wf_first = nullptr, wf_next = nullptr;
+    {
+        const char* e = getenv("ZRT_WF_MINW");     // tuning sweeps only
+        const int mw = e ? atoi(e) : (split ? kSplitMinWaves : kWfMinWaves);
+#define ZRT_WF_PICK(K, MW)                                                   \
+    do {                                                                     \
+        wf_first = (WfFn)K<kTriBatch, MW, true>;                             \
+        wf_next = (WfFn)K<kTriBatch, MW, false>;                             \
+    } while (0)
+#define ZRT_WF_SWITCH(K)                                                     \
+    switch (mw) {                                                            \
+        case 4: ZRT_WF_PICK(K, 4); break;                                    \
+        case 5: ZRT_WF_PICK(K, 5); break;                                    \
+        case 6: ZRT_WF_PICK(K, 6); break;                                    \
+        case 7: ZRT_WF_PICK(K, 7); break;                                    \
+        default: ZRT_WF_PICK(K, 8); break;                                   \
+    }
+        if (split) { ZRT_WF_SWITCH(wf_trace_kernel) } else { ZRT_WF_SWITCH(wf_kernel) }
+#undef ZRT_WF_SWITCH
+#undef ZRT_WF_PICK
     }
     uint32_t grid_blocks = 0, grid_first = 0, grid_next = 0;
     if (wf) {
@@ -951,6 +1157,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     } else if ((rc = grid_for((const void*)fn, &grid_blocks)) != ZRT_OK) {
         return rc;
     }
+    uint32_t refill = 48;
+    if (const char* e = getenv("ZRT_REFILL")) refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    const uint32_t shade_blocks = (uint32_t)c->num_cus * 8u;
 
     TraceParams tp;
     memset(&tp, 0, sizeof tp);
@@ -988,7 +1197,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
-    uint32_t launches = 0;
+    uint32_t launches = 0, ne = 0;
     for (uint32_t pass = 0; pass < npasses; ++pass) {
         const uint32_t s0 = (uint32_t)(pass * s_pass);
         const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
@@ -1004,8 +1213,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.t = tp;
             W.stk = c->d_stk;
             W.term = c->d_term;
+            W.hit = c->d_hit;
             W.T = (uint32_t)T;
-            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
+            W.refill = refill;
             const uint32_t nb = std::max<uint32_t>(mb, 1);
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
@@ -1013,24 +1223,34 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.n_in = n + k;
                 W.n_out = n + k + 1;
                 W.fetch = fetch + k;
-                if (k == 0)
-                    hipLaunchKernelGGL(wf_first, dim3(grid_first), dim3(tblock), lds_bytes, c->stream, W);
-                else
-                    hipLaunchKernelGGL(wf_next, dim3(grid_next), dim3(tblock), lds_bytes, c->stream, W);
-                HIP_TRY(hipGetLastError());
-                ++launches;
+                if (!split || mb > 0) {
+                    HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                    if (k == 0)
+                        hipLaunchKernelGGL(wf_first, dim3(grid_first), dim3(tblock), lds_bytes, c->stream, W);
+                    else
+                        hipLaunchKernelGGL(wf_next, dim3(grid_next), dim3(tblock), lds_bytes, c->stream, W);
+                    HIP_TRY(hipGetLastError());
+                    HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                    ++launches;
+                }
+                if (split) {
+                    if (k == 0)
+                        hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
+                    else
+                        hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
+                    HIP_TRY(hipGetLastError());
+                }
             }
-            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
             hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
                                c->d_term, c->d_stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
                                c->d_rgb, want_lin ? c->d_lin : nullptr);
         } else {
             HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
-            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass], c->stream));
+            HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
             hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tblock), lds_bytes, c->stream, tp);
             HIP_TRY(hipGetLastError());
             ++launches;
-            HIP_TRY(hipEventRecord(c->ev_trace[2 * pass + 1], c->stream));
+            HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
             hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
                                c->d_out, P, S, c->d_acc, first, last, inv_spp, c->d_rgb,
                                want_lin ? c->d_lin : nullptr);
@@ -1049,12 +1269,15 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         fprintf(stderr, "{\"zrt_profile_wave_cycles\": {\"cell_tris\": %llu, \"dda\": %llu, "
                 "\"trace\": %llu, \"shade\": %llu, \"fetch\": %llu, \"total\": %llu}}\n",
                 hs[8], hs[9], hs[10], hs[11], hs[12], hs[13]);
+    if (getenv("ZRT_CELL_STATS") && want_stats)
+        fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu}}\n",
+                hs[1], hs[4], hs[5]);
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
-    for (uint32_t pass = 0; pass < npasses; ++pass) {
+    for (uint32_t e = 0; e + 1 < ne; e += 2) {   // trace launches only (not shade / resolve)
         float t = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[2 * pass], c->ev_trace[2 * pass + 1]));
+        HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[e], c->ev_trace[e + 1]));
         st.trace_kernel_ms += t;
     }
     st.trace_launches = launches;
