@@ -1,0 +1,136 @@
+// Host check of BRICK_SKIP4 (csrc/dda.h): on random grids, occupancies and
+// rays (including axis-aligned and exact-diagonal ones that produce crossing
+// ties), the skip walk must enter exactly the same cells of occupied bricks,
+// with bit-identical DDA state, as the cell-by-cell walk of Iterator.next
+// (DDA_STEP), and leave the grid at the same point.
+//   g++ -O2 -std=c++17 -ffp-contract=off -I<csrc> dda_skip_check.cpp
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "dda.h"
+
+using namespace zrt;
+
+struct TestGrid {
+    float bmin[3], bmax[3], cs[3];
+    uint32_t res[3];
+    uint32_t nb[3];
+    std::vector<uint8_t> occ;   // per 4^3 brick
+    bool occupied(uint32_t c0, uint32_t c1, uint32_t c2) const {
+        return occ[((c2 >> 2) * nb[1] + (c1 >> 2)) * nb[0] + (c0 >> 2)] != 0;
+    }
+};
+
+struct Rec {
+    uint32_t c0, c1, c2, lin;
+    float tn0, tn1, tn2;
+    bool operator==(const Rec& o) const {
+        return c0 == o.c0 && c1 == o.c1 && c2 == o.c2 && lin == o.lin &&
+               !memcmp(&tn0, &o.tn0, 4) && !memcmp(&tn1, &o.tn1, 4) && !memcmp(&tn2, &o.tn2, 4);
+    }
+};
+
+static Rec rec(const Dda& s) { return Rec{s.c0, s.c1, s.c2, s.lin, s.tn0, s.tn1, s.tn2}; }
+
+// reference: every cell; keep the ones in occupied bricks
+static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
+    std::vector<Rec> out;
+    for (int guard = 0; guard < 100000; ++guard) {
+        if (g.occupied(s.c0, s.c1, s.c2)) out.push_back(rec(s));
+        bool crossed;
+        float t_exit;
+        DDA_STEP(s, k, 2, crossed, t_exit);
+        (void)crossed;
+        if (t_exit == kInf) return out;
+    }
+    out.push_back(Rec{~0u, ~0u, ~0u, ~0u, 0, 0, 0});
+    return out;
+}
+
+// product: skip unoccupied bricks whole
+static std::vector<Rec> walk_skip(const TestGrid& g, const GridK& k, Dda s, uint64_t* skips) {
+    std::vector<Rec> out;
+    for (int guard = 0; guard < 100000; ++guard) {
+        const bool occ = g.occupied(s.c0, s.c1, s.c2);
+        if (!occ && s.neg < 8u) {
+            bool exited;
+            BRICK_SKIP4(s, k, exited);
+            ++*skips;
+            if (exited) return out;
+            continue;
+        }
+        if (occ) out.push_back(rec(s));
+        bool crossed;
+        float t_exit;
+        DDA_STEP(s, k, 2, crossed, t_exit);
+        (void)crossed;
+        if (t_exit == kInf) return out;
+    }
+    out.push_back(Rec{~0u, ~0u, ~0u, ~0u, 0, 0, 0});
+    return out;
+}
+
+int main(int argc, char** argv) {
+    const int n_grids = argc > 1 ? atoi(argv[1]) : 40;
+    const int n_rays = argc > 2 ? atoi(argv[2]) : 4000;
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<float> U(0.0f, 1.0f);
+    uint64_t total = 0, skips = 0, ties = 0, fails = 0;
+    for (int gi = 0; gi < n_grids; ++gi) {
+        TestGrid g;
+        const bool pow2 = gi % 3 == 0;     // exact arithmetic -> many crossing ties
+        for (int a = 0; a < 3; ++a) {
+            g.res[a] = gi == 0 ? 128u : 1u + (uint32_t)(rng() % 40);
+            g.bmin[a] = pow2 ? 0.0f : -5.0f + 10.0f * U(rng);
+            g.cs[a] = pow2 ? 0.25f : 0.05f + U(rng);
+            g.bmax[a] = g.bmin[a] + g.cs[a] * (float)g.res[a];
+            g.nb[a] = (g.res[a] + 3) / 4;
+        }
+        g.occ.resize((size_t)g.nb[0] * g.nb[1] * g.nb[2]);
+        const float dens = (gi % 4) * 0.1f;
+        for (auto& o : g.occ) o = U(rng) < dens;
+        GridK k{g.res[0] - 1, g.res[1] - 1, g.res[2] - 1, g.res[0], g.res[0] * g.res[1]};
+        for (int r = 0; r < n_rays; ++r) {
+            v3 o, d;
+            const int kind = r % 4;
+            float c[3];
+            for (int a = 0; a < 3; ++a) {
+                const float ext = g.bmax[a] - g.bmin[a];
+                c[a] = g.bmin[a] - 0.5f * ext + 2.0f * ext * U(rng);
+                if (kind >= 2) c[a] = g.bmin[a] + g.cs[a] * (float)(rng() % (g.res[a] + 1));   // on cell corners
+            }
+            o = mk(c[0], c[1], c[2]);
+            if (kind == 0) {
+                d = normalize(mk(U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f));
+            } else if (kind == 1) {                 // one or two zero components
+                float v[3] = {U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f};
+                v[rng() % 3] = 0.0f;
+                if (rng() & 1) v[rng() % 3] = 0.0f;
+                if (v[0] == 0 && v[1] == 0 && v[2] == 0) v[0] = 1.0f;
+                d = normalize(mk(v[0], v[1], v[2]));
+            } else {                                // exact diagonals: equal |d| per axis
+                const float sx = (rng() & 1) ? 1.0f : -1.0f, sy = (rng() & 1) ? 1.0f : -1.0f,
+                            sz = (rng() & 1) ? 1.0f : -1.0f;
+                d = kind == 2 ? normalize(mk(sx, sy, sz)) : normalize(mk(sx, 2.0f * sy, sz));
+            }
+            Dda s;
+            if (!dda_init(g.bmin, g.bmax, g.res, g.cs, o, d, s)) continue;
+            ++total;
+            if (s.tn0 == s.tn1 || s.tn1 == s.tn2 || s.tn0 == s.tn2) ++ties;
+            const auto a = walk_cells(g, k, s);
+            const auto b = walk_skip(g, k, s, &skips);
+            if (!(a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin()))) {
+                if (++fails <= 5)
+                    fprintf(stderr, "MISMATCH grid %d ray %d: %zu vs %zu cells (o=%g,%g,%g d=%g,%g,%g)\n", gi, r,
+                            a.size(), b.size(), o.x, o.y, o.z, d.x, d.y, d.z);
+            }
+        }
+    }
+    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"fails\": %llu}\n",
+           (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
+           (unsigned long long)fails);
+    return fails ? 1 : 0;
+}

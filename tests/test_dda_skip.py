@@ -1,0 +1,25 @@
+"""Host check of the exact empty-brick skip (csrc/dda.h BRICK_SKIP4) against
+the cell-by-cell Iterator.next walk (DDA_STEP): same cells of occupied
+bricks, bit-identical DDA state, same grid exit (tests/cpp/dda_skip_check.cpp).
+The GPU kernels compile the same header; their images are checked against
+the oracle in test_gpu_parity.py."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_brick_skip_matches_cell_walk(tmp_path):
+    exe = tmp_path / "ddachk"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+                    "-I", os.path.join(ROOT, "zig_raytracing_contest_amd", "csrc"),
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "dda_skip_check.cpp"), "-o", str(exe)],
+                   check=True)
+    r = subprocess.run([str(exe), "60", "6000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert '"fails": 0' in r.stdout

@@ -1,0 +1,148 @@
+// Uniform-grid DDA (Grid.traceRay / Grid.Iterator, linalg.zig:443-496) and
+// the exact empty-brick skip, shared by the HIP kernels (render.hip) and the
+// host-side check tests/cpp/dda_skip_check.cpp (g++ -ffp-contract=off).
+#pragma once
+#include <stdint.h>
+
+#include "zrt_math.h"
+
+namespace zrt {
+
+ZHD uint32_t zmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// Grid.Iterator state (linalg.zig:471-477) + the running cell index.  The
+// exit cell, step and linear-index step of each axis follow from the sign of
+// the ray direction (linalg.zig:450-452), kept as 3 bits in `neg`.
+struct Dda {
+    float tn0, tn1, tn2, td0, td1, td2;
+    uint32_t c0, c1, c2;
+    uint32_t lin;
+    uint32_t neg;             // bit a: dir[a] < 0
+};
+
+// Grid.traceRay (linalg.zig:443-469); false if the ray misses the grid bbox.
+ZHD bool dda_init(const float* bmin, const float* bmax, const uint32_t* res, const float* cs, v3 o, v3 d,
+                  Dda& s) {
+    Bbox bb;
+    bb.min = mk(bmin[0], bmin[1], bmin[2]);
+    bb.max = mk(bmax[0], bmax[1], bmax[2]);
+    float t_hit;
+    if (!bbox_ray(bb, o, d, &t_hit)) return false;
+    t_hit = fmaxf(0.0f, t_hit);
+    const v3 local = sub(add(o, scale(d, t_hit)), bb.min);
+    const bool n0 = d.x < 0.0f, n1 = d.y < 0.0f, n2 = d.z < 0.0f;
+    s.c0 = zmin(f2u(local.x / cs[0]), res[0] - 1u);
+    s.c1 = zmin(f2u(local.y / cs[1]), res[1] - 1u);
+    s.c2 = zmin(f2u(local.z / cs[2]), res[2] - 1u);
+    s.neg = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
+    s.td0 = fabsf(cs[0] / d.x);
+    s.td1 = fabsf(cs[1] / d.y);
+    s.td2 = fabsf(cs[2] / d.z);
+    s.tn0 = t_hit + ((((float)(s.c0 + (n0 ? 0u : 1u))) * cs[0] - local.x) / d.x);
+    s.tn1 = t_hit + ((((float)(s.c1 + (n1 ? 0u : 1u))) * cs[1] - local.y) / d.y);
+    s.tn2 = t_hit + ((((float)(s.c2 + (n2 ? 0u : 1u))) * cs[2] - local.z) / d.z);
+    s.lin = (s.c2 * res[1] + s.c1) * res[0] + s.c0;
+    // bit 3: some crossing sequence starts at -inf / NaN (a zero direction
+    // component on a boundary), where BRICK_SKIP4's merge argument fails
+    const bool ok = s.tn0 > -kInf && s.tn1 > -kInf && s.tn2 > -kInf && s.td0 == s.td0 && s.td1 == s.td1 &&
+                    s.td2 == s.td2;
+    s.neg |= ok ? 0u : 8u;
+    return true;
+}
+
+// Iterator.next (linalg.zig:478-496), branch-free.  map[k] with
+// k = (t0<t1)<<2 | (t0<t2)<<1 | (t1<t2) and map = {2,1,2,1,2,2,0,0} is
+// exactly: axis 0 iff t0<t1 && t0<t2; axis 1 iff !(t0<t1) && t1<t2; else 2
+// (same booleans, so NaNs pick the same axis).  T_EXIT = the crossing t of
+// the chosen axis, or +inf at the exit cell.  On that +inf the state is
+// stepped past the exit, which is harmless: traceRay always stops there
+// (nearest <= inf).  CROSSED: the step left the current occupancy brick.
+// A macro over a local Dda, not a function on a reference: as a function,
+// InstCombine turns `a0 ? s.c0 : s.c1` into a load through a selected
+// pointer and the whole state lands in scratch memory.  For the same reason
+// the grid constants come in as a GridK of laundered registers: selecting
+// between res[0..2] directly became a global load from the kernel
+// arguments at a selected offset, i.e. a memory round trip in every step.
+struct GridK {
+    uint32_t rm0, rm1, rm2;   // res[k] - 1: last cell index per axis
+    uint32_t str1, str2;      // linear-index strides of axes 1 and 2
+};
+#define DDA_STEP(S, G, SH, CROSSED, T_EXIT)                                           \
+    do {                                                                             \
+        const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
+        const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
+        const bool a0_ = b01_ && b02_;                                               \
+        const bool a1_ = !b01_ && b12_;                                              \
+        const bool a2_ = !a0_ && !a1_;                                               \
+        const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
+        const uint32_t c0_ = (S).c0, c1_ = (S).c1, c2_ = (S).c2;                     \
+        const uint32_t cc_ = a0_ ? c0_ : (a1_ ? c1_ : c2_);                          \
+        const uint32_t ax_ = a0_ ? 0u : (a1_ ? 1u : 2u);                             \
+        const bool ng_ = ((S).neg >> ax_) & 1u;                                      \
+        const uint32_t rm1_ = a0_ ? (G).rm0 : (a1_ ? (G).rm1 : (G).rm2);           \
+        const uint32_t ec_ = ng_ ? 0u : rm1_;                                        \
+        const uint32_t cn_ = ng_ ? cc_ - 1u : cc_ + 1u;                              \
+        const uint32_t str_ = a0_ ? 1u : (a1_ ? (G).str1 : (G).str2);             \
+        (CROSSED) = ((cc_ ^ cn_) >> (SH)) != 0u;                                     \
+        const float u0_ = t0_ + (S).td0, u1_ = t1_ + (S).td1, u2_ = t2_ + (S).td2;   \
+        (S).tn0 = a0_ ? u0_ : t0_;                                                   \
+        (S).tn1 = a1_ ? u1_ : t1_;                                                   \
+        (S).tn2 = a2_ ? u2_ : t2_;                                                   \
+        (S).c0 = a0_ ? cn_ : c0_;                                                    \
+        (S).c1 = a1_ ? cn_ : c1_;                                                    \
+        (S).c2 = a2_ ? cn_ : c2_;                                                    \
+        (S).lin = ng_ ? (S).lin - str_ : (S).lin + str_;                             \
+        (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
+    } while (0)
+
+// Empty-brick skip, 4^3 bricks (occ_shift 2): the state Iterator.next would
+// reach at the step that leaves the current brick, computed at once.  Axis
+// a's crossings form the sequence T_a(1) = tn_a, T_a(j+1) = T_a(j) + td_a
+// (the same f32 adds the DDA does); Iterator.next always takes the smallest
+// head, ties to the higher axis (DDA_STEP's booleans), so the steps are the
+// merge of the three sequences ordered by (t, -axis).  The brick is left by
+// the first, in that order, of the brick-exit crossings E_a = T_a(m_a)
+// (m_a = cells to the brick face along a), and every other axis b has then
+// taken exactly the crossings T_b(j), j < m_b, that precede it.  Only used
+// while nothing is hit yet (nearest = inf: no cell of an empty brick can end
+// the walk except the grid exit) and with no -inf/NaN sequence (neg bit 3).
+// EXITED: the skip left the grid (traceRay returns no hit).
+#define SKIP_AXIS(S, G, A)                                                                    \
+    const bool n##A##_ = ((S).neg >> A) & 1u;                                                 \
+    const uint32_t lo##A##_ = (S).c##A & ~3u;                                                 \
+    const uint32_t hi##A##_ = zmin(lo##A##_ + 3u, (G).rm##A);                                  \
+    const uint32_t m##A##_ = n##A##_ ? (S).c##A - lo##A##_ + 1u : hi##A##_ - (S).c##A + 1u;   \
+    const bool out##A##_ = n##A##_ ? lo##A##_ == 0u : hi##A##_ == (G).rm##A;                  \
+    const float T##A##1_ = (S).tn##A;                                                         \
+    const float T##A##2_ = T##A##1_ + (S).td##A;                                              \
+    const float T##A##3_ = T##A##2_ + (S).td##A;                                              \
+    const float T##A##4_ = T##A##3_ + (S).td##A;                                              \
+    const float E##A##_ = m##A##_ == 1u ? T##A##1_                                            \
+                        : (m##A##_ == 2u ? T##A##2_ : (m##A##_ == 3u ? T##A##3_ : T##A##4_));
+#define SKIP_COUNT(S, A, TIE)                                                                 \
+    uint32_t k##A##_ = 0;                                                                     \
+    k##A##_ += (1u < m##A##_ && (T##A##1_ < ex_ || (T##A##1_ == ex_ && (TIE)))) ? 1u : 0u;     \
+    k##A##_ += (2u < m##A##_ && (T##A##2_ < ex_ || (T##A##2_ == ex_ && (TIE)))) ? 1u : 0u;     \
+    k##A##_ += (3u < m##A##_ && (T##A##3_ < ex_ || (T##A##3_ == ex_ && (TIE)))) ? 1u : 0u;     \
+    k##A##_ = x##A##_ ? m##A##_ : k##A##_;                                                    \
+    (S).tn##A = k##A##_ == 0u ? T##A##1_                                                      \
+              : (k##A##_ == 1u ? T##A##2_                                                     \
+              : (k##A##_ == 2u ? T##A##3_ : (k##A##_ == 3u ? T##A##4_ : T##A##4_ + (S).td##A))); \
+    (S).c##A = n##A##_ ? (S).c##A - k##A##_ : (S).c##A + k##A##_;
+#define BRICK_SKIP4(S, G, EXITED)                                                             \
+    do {                                                                                      \
+        SKIP_AXIS(S, G, 0)                                                                    \
+        SKIP_AXIS(S, G, 1)                                                                    \
+        SKIP_AXIS(S, G, 2)                                                                    \
+        const bool x0_ = E0_ < E1_ && E0_ < E2_;                                              \
+        const bool x1_ = !(E0_ < E1_) && E1_ < E2_;                                           \
+        const bool x2_ = !x0_ && !x1_;                                                        \
+        const float ex_ = x0_ ? E0_ : (x1_ ? E1_ : E2_);                                      \
+        SKIP_COUNT(S, 0, false)                                                               \
+        SKIP_COUNT(S, 1, x0_)                                                                 \
+        SKIP_COUNT(S, 2, !x2_)                                                                \
+        (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                       \
+        (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
+    } while (0)
+
+}  // namespace zrt

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "zrt_internal.h"
+#include "dda.h"
 
 using namespace zrt;
 
@@ -113,57 +114,10 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
-// Grid.Iterator state (linalg.zig:471-477) + the running cell index.  The
-// exit cell, step and linear-index step of each axis follow from the sign of
-// the ray direction (linalg.zig:450-452), kept as 3 bits in `neg`.
-struct Dda {
-    float tn0, tn1, tn2, td0, td1, td2;
-    uint32_t c0, c1, c2;
-    uint32_t lin;
-    uint32_t neg;             // bit a: dir[a] < 0
-};
-
-// Grid.traceRay (linalg.zig:443-469); false if the ray misses the grid bbox.
 __device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda& s) {
-    Bbox bb;
-    bb.min = mk(p.bmin[0], p.bmin[1], p.bmin[2]);
-    bb.max = mk(p.bmax[0], p.bmax[1], p.bmax[2]);
-    float t_hit;
-    if (!bbox_ray(bb, o, d, &t_hit)) return false;
-    t_hit = fmaxf(0.0f, t_hit);
-    const v3 local = sub(add(o, scale(d, t_hit)), bb.min);
-    const bool n0 = d.x < 0.0f, n1 = d.y < 0.0f, n2 = d.z < 0.0f;
-    s.c0 = min(f2u(local.x / p.cs[0]), p.res[0] - 1u);
-    s.c1 = min(f2u(local.y / p.cs[1]), p.res[1] - 1u);
-    s.c2 = min(f2u(local.z / p.cs[2]), p.res[2] - 1u);
-    s.neg = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
-    s.td0 = fabsf(p.cs[0] / d.x);
-    s.td1 = fabsf(p.cs[1] / d.y);
-    s.td2 = fabsf(p.cs[2] / d.z);
-    s.tn0 = t_hit + ((((float)(s.c0 + (n0 ? 0u : 1u))) * p.cs[0] - local.x) / d.x);
-    s.tn1 = t_hit + ((((float)(s.c1 + (n1 ? 0u : 1u))) * p.cs[1] - local.y) / d.y);
-    s.tn2 = t_hit + ((((float)(s.c2 + (n2 ? 0u : 1u))) * p.cs[2] - local.z) / d.z);
-    s.lin = (s.c2 * p.res[1] + s.c1) * p.res[0] + s.c0;
-    return true;
+    return dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s);
 }
-
-// Iterator.next (linalg.zig:478-496), branch-free.  map[k] with
-// k = (t0<t1)<<2 | (t0<t2)<<1 | (t1<t2) and map = {2,1,2,1,2,2,0,0} is
-// exactly: axis 0 iff t0<t1 && t0<t2; axis 1 iff !(t0<t1) && t1<t2; else 2
-// (same booleans, so NaNs pick the same axis).  T_EXIT = the crossing t of
-// the chosen axis, or +inf at the exit cell.  On that +inf the state is
-// stepped past the exit, which is harmless: traceRay always stops there
-// (nearest <= inf).  CROSSED: the step left the current occupancy brick.
-// A macro over a local Dda, not a function on a reference: as a function,
-// InstCombine turns `a0 ? s.c0 : s.c1` into a load through a selected
-// pointer and the whole state lands in scratch memory.  For the same reason
-// the grid constants come in as a GridK of laundered registers: selecting
-// between p.res[0..2] directly became a global load from the kernel
-// arguments at a selected offset, i.e. a memory round trip in every step.
-struct GridK {
-    uint32_t rm0, rm1, rm2;   // res[k] - 1: last cell index per axis
-    uint32_t str1, str2;      // linear-index strides of axes 1 and 2
-};
+// Grid constants as wave-uniform registers (see GridK).
 __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     GridK g;
     g.rm0 = __builtin_amdgcn_readfirstlane(p.res[0] - 1u);
@@ -173,33 +127,6 @@ __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     g.str2 = __builtin_amdgcn_readfirstlane(p.res[0] * p.res[1]);
     return g;
 }
-#define DDA_STEP(S, G, SH, CROSSED, T_EXIT)                                           \
-    do {                                                                             \
-        const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
-        const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
-        const bool a0_ = b01_ && b02_;                                               \
-        const bool a1_ = !b01_ && b12_;                                              \
-        const bool a2_ = !a0_ && !a1_;                                               \
-        const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
-        const uint32_t c0_ = (S).c0, c1_ = (S).c1, c2_ = (S).c2;                     \
-        const uint32_t cc_ = a0_ ? c0_ : (a1_ ? c1_ : c2_);                          \
-        const uint32_t ax_ = a0_ ? 0u : (a1_ ? 1u : 2u);                             \
-        const bool ng_ = ((S).neg >> ax_) & 1u;                                      \
-        const uint32_t rm1_ = a0_ ? (G).rm0 : (a1_ ? (G).rm1 : (G).rm2);           \
-        const uint32_t ec_ = ng_ ? 0u : rm1_;                                        \
-        const uint32_t cn_ = ng_ ? cc_ - 1u : cc_ + 1u;                              \
-        const uint32_t str_ = a0_ ? 1u : (a1_ ? (G).str1 : (G).str2);             \
-        (CROSSED) = ((cc_ ^ cn_) >> (SH)) != 0u;                                     \
-        const float u0_ = t0_ + (S).td0, u1_ = t1_ + (S).td1, u2_ = t2_ + (S).td2;   \
-        (S).tn0 = a0_ ? u0_ : t0_;                                                   \
-        (S).tn1 = a1_ ? u1_ : t1_;                                                   \
-        (S).tn2 = a2_ ? u2_ : t2_;                                                   \
-        (S).c0 = a0_ ? cn_ : c0_;                                                    \
-        (S).c1 = a1_ ? cn_ : c1_;                                                    \
-        (S).c2 = a2_ ? cn_ : c2_;                                                    \
-        (S).lin = ng_ ? (S).lin - str_ : (S).lin + str_;                             \
-        (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
-    } while (0)
 
 // All triangles of one cell in reference order (stage3.zig:164-178), TB at
 // a time: the TB loads are issued before the first test so their latencies
@@ -207,8 +134,10 @@ __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
 template <int TB, bool STATS>
 __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
                                           float& nearest, float& hu, float& hv, uint32_t& hidx,
-                                          uint32_t& n_tests) {
+                                          uint32_t& n_tests, uint64_t* wstat = nullptr) {
     for (uint32_t i = b; i < e; i += TB) {
+        // counting build: wave trips of this loop (first active lane counts)
+        if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++wstat[1];
         float4 A[TB], B[TB], Cc[TB];
 #pragma unroll
         for (int k = 0; k < TB; ++k) {
@@ -243,7 +172,7 @@ __device__ __forceinline__ uint64_t stamp() {
 // nothing in the result: the DDA arithmetic runs for every cell exactly as
 // Iterator.next does; only the 8-byte Cell load is skipped when the cell's
 // brick holds no triangle (its range would be empty).
-template <bool STATS, bool PROF, int TB>
+template <bool STATS, bool PROF, int TB, bool SKIP = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof) {
@@ -257,12 +186,20 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         uint64_t ta = 0, tb = 0;
         if (PROF) ta = stamp();
         if (STATS) ++n_cells;
+        if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++prof[8];
         if (occupied) {
             const uint2 cell = p.cells[s.lin];
             if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; }
-            test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests);
+            test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8);
         }
         if (PROF) tb = stamp();
+        if (SKIP && !occupied && nearest == kInf && s.neg < 8u) {
+            bool exited;
+            BRICK_SKIP4(s, gk, exited);
+            if (exited) break;
+            occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
+            continue;
+        }
         bool crossed;
         float t_exit;
         DDA_STEP(s, gk, sh, crossed, t_exit);
@@ -305,7 +242,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
     // cell+tris, dda, trace, shade, fetch, total (PROF); cell loads, non-empty cells (STATS)
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // + wave trips of the cell loop / triangle-batch loop (STATS)
+    uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_begin = PROF ? stamp() : 0;
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
@@ -392,6 +330,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     if (STATS) {
         s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits);
         s4 = wave_sum(prof[6]); s5 = wave_sum(prof[7]);
+        const unsigned long long s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]);
+        if (lane == 0) { atomicAdd(&p.stats[6], s6); atomicAdd(&p.stats[7], s7); }
     }
     if (lane == 0) {
         atomicAdd(&p.stats[0], s0);
@@ -512,7 +452,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
     }
 }
 
-template <int TB, int MINW, bool PRIMARY>
+template <int TB, int MINW, bool PRIMARY, bool SKIP = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -526,7 +466,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
     const uint32_t n = PRIMARY ? p.total : *w.n_in;
     uint32_t n_seg = 0, dummy = 0;
-    uint64_t prof_dummy[2];
+    uint64_t prof_dummy[10];
 
     for (;;) {
         uint32_t base = 0;
@@ -563,8 +503,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
                 ++n_seg;
                 float hu = 0.0f, hv = 0.0f;
                 uint32_t hidx = 0;
-                const float t = trace_ray<false, false, TB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy,
-                                                            prof_dummy);
+                const float t = trace_ray<false, false, TB, SKIP>(p, s_occ, o, d, hu, hv, hidx, dummy,
+                                                                  dummy, prof_dummy);
                 cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
             }
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
@@ -1146,7 +1086,15 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         case 7: ZRT_WF_PICK(K, 7); break;                                    \
         default: ZRT_WF_PICK(K, 8); break;                                   \
     }
-        if (split) { ZRT_WF_SWITCH(wf_trace_kernel) } else { ZRT_WF_SWITCH(wf_kernel) }
+        const char* sk = getenv("ZRT_SKIP");
+        if (split) {
+            ZRT_WF_SWITCH(wf_trace_kernel)
+        } else if (c->occ_shift == 2 && sk && atoi(sk) == 1) {
+            if (mw == 5) { wf_first = (WfFn)wf_kernel<kTriBatch, 5, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 5, false, true>; }
+            else { wf_first = (WfFn)wf_kernel<kTriBatch, 6, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 6, false, true>; }
+        } else {
+            ZRT_WF_SWITCH(wf_kernel)
+        }
 #undef ZRT_WF_SWITCH
 #undef ZRT_WF_PICK
     }
@@ -1270,8 +1218,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 "\"trace\": %llu, \"shade\": %llu, \"fetch\": %llu, \"total\": %llu}}\n",
                 hs[8], hs[9], hs[10], hs[11], hs[12], hs[13]);
     if (getenv("ZRT_CELL_STATS") && want_stats)
-        fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu}}\n",
-                hs[1], hs[4], hs[5]);
+        fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu, "
+                "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu}}\n",
+                hs[1], hs[4], hs[5], hs[2], hs[6], hs[7]);
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
