@@ -41,6 +41,23 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 B_CELL, B_TRI, B_HIT, B_PIX = 8, 36, 64 + 4 * (12 + 12 + 4), 3
 
 
+def traffic_for(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary for this
+    workload (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of this bench; gfx950 corrections there), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json"))):
+        try:
+            with open(f) as fh:
+                t = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if t.get("kernel") == kernel:
+            best = (t["bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,6 +178,8 @@ def main():
         # achieved = sum(bytes) / sum(launch durations) over the step.
         per_launch = alg_bytes / max(launches / a.steps, 1)
         achieved = per_launch / avg_launch_s / 1e9
+        mode = os.environ.get("ZRT_MODE", "wf")
+        kname = {"mega": "trace_kernel", "split": "wf_trace_kernel"}.get(mode, "wf_kernel")
         out = {
             "metric": "Mrays/sec + wall-clock to output.png on contest config.json scene",
             "value": round(total_segs / elapsed / 1e6, 3),
@@ -178,11 +197,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": None,
-                         "kernel": os.environ.get("ZRT_MODE", "wf") == "mega" and "trace_kernel" or "wf_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "kernel": kname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "alg_bytes_per_launch": int(per_launch)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},
         }
+        tr = traffic_for(a.config, kname) if spp == cfgd["spp"] else None
+        if tr:
+            out["roofline"]["traffic"] = round(tr[0] / 1e9, 3)
+            out["roofline"]["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            out["roofline"]["traffic_source"] = tr[1]
+            out["roofline"]["alg_GB_per_launch"] = round(per_launch / 1e9, 3)
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(soup, cfgd, a.cpu_seconds)
             out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)

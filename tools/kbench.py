@@ -48,9 +48,14 @@ for var in (a.var or [""]):
     same = True if ref is None else bool(np.array_equal(ref, img))
     if ref is None:
         ref = img.copy()
-    print(json.dumps({"var": var or "default", "mrays": round(st["segments"] / min(ts) / 1e6, 1),
-                      "kernel_ms": round(st["trace_kernel_ms"], 2), "wall_ms": round(min(ts) * 1e3, 2),
-                      "identical": same}), flush=True)
+    rec = {"var": var or "default", "mrays": round(st["segments"] / min(ts) / 1e6, 1),
+           "kernel_ms": round(st["trace_kernel_ms"], 2), "wall_ms": round(min(ts) * 1e3, 2),
+           "identical": same, "segments": int(st["segments"])}
+    if not same:
+        dif = np.any(ref != img, axis=2)
+        rec["diff_pixels"] = int(dif.sum())
+        rec["max_abs"] = int(np.abs(ref.astype(int) - img.astype(int)).max())
+    print(json.dumps(rec), flush=True)
     ctx.close()
     for k, v in old.items():
         if v is None:

@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <unordered_map>
 #include <vector>
 
 #include "zrt_internal.h"
@@ -128,13 +129,31 @@ __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     return g;
 }
 
+// Mailbox of the last 4 triangle shapes tested by this ray segment.  The
+// bake copies a triangle into every cell it overlaps (5.6 copies each on the
+// contest stand-in), so a ray walking along a large triangle re-tests the
+// same vertices cell after cell.  A re-test cannot change the result:
+// acceptance depends only on t (nearest > t && t > 0, stage3.zig:172) and t
+// only on the vertices and the ray; if the first test set nearest = t the
+// re-test fails nearest > t, if it failed it fails again (nearest only
+// shrinks).  So a ref whose shape id (tri_pos[3j].w: equal positions ->
+// equal id, assigned at context creation) is in the mailbox is skipped.
+struct Mailbox {
+    uint32_t m0, m1, m2, m3;
+    __device__ __forceinline__ void reset() { m0 = m1 = m2 = m3 = 0xFFFFFFFFu; }
+    __device__ __forceinline__ bool has(uint32_t id) const { return id == m0 || id == m1 || id == m2 || id == m3; }
+    __device__ __forceinline__ void push(uint32_t id) { m3 = m2; m2 = m1; m1 = m0; m0 = id; }
+};
+
 // All triangles of one cell in reference order (stage3.zig:164-178), TB at
 // a time: the TB loads are issued before the first test so their latencies
 // overlap (one memory round trip per TB triangles instead of per triangle).
-template <int TB, bool STATS>
+// MB: mailbox skipping (see Mailbox); the counting build (STATS) tests every
+// ref as the reference does and only counts the ones MB would skip.
+template <int TB, bool STATS, bool MB = false>
 __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
                                           float& nearest, float& hu, float& hv, uint32_t& hidx,
-                                          uint32_t& n_tests, uint64_t* wstat = nullptr) {
+                                          uint32_t& n_tests, uint64_t* wstat, Mailbox& mbx) {
     for (uint32_t i = b; i < e; i += TB) {
         // counting build: wave trips of this loop (first active lane counts)
         if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++wstat[1];
@@ -148,7 +167,15 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
         }
 #pragma unroll
         for (int k = 0; k < TB; ++k) {
-            if (i + (uint32_t)k < e) {
+            bool live = i + (uint32_t)k < e;
+            if (MB || STATS) {
+                const uint32_t id = __float_as_uint(A[k].w);
+                const bool seen = mbx.has(id);
+                (void)seen;
+                if (MB) live = live && !seen;
+                if (live) mbx.push(id);
+            }
+            if (live) {
                 if (STATS) ++n_tests;
                 float t, u, v;
                 if (tri_ray(mk(A[k].x, A[k].y, A[k].z), mk(B[k].x, B[k].y, B[k].z),
@@ -172,11 +199,13 @@ __device__ __forceinline__ uint64_t stamp() {
 // nothing in the result: the DDA arithmetic runs for every cell exactly as
 // Iterator.next does; only the 8-byte Cell load is skipped when the cell's
 // brick holds no triangle (its range would be empty).
-template <bool STATS, bool PROF, int TB, bool SKIP = false>
+template <bool STATS, bool PROF, int TB, bool MB = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
-                                           uint32_t& n_tests, uint64_t* prof) {
+                                           uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr) {
     float nearest = kInf;
+    Mailbox mbx;
+    mbx.reset();
     Dda s;
     if (!dda_setup(p, o, d, s)) return nearest;
     const uint32_t sh = p.occ_shift;
@@ -187,25 +216,150 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         if (PROF) ta = stamp();
         if (STATS) ++n_cells;
         if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++prof[8];
+        uint32_t ncell = 0;
         if (occupied) {
             const uint2 cell = p.cells[s.lin];
-            if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; }
-            test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8);
+            if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; ncell = cell.y - cell.x; }
+            test_cell<TB, STATS, MB>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8, mbx);
+        }
+        if (STATS) {
+            // wave-shared work of this trip: sum of the lanes' triangle counts
+            // -> trips with any test, and 64-wide rounds if shared evenly
+            uint32_t* wc = wcnt + 2 * (threadIdx.x >> 6);
+            const bool first = (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1));
+            if (first) wc[0] = 0;
+            __builtin_amdgcn_wave_barrier();
+            atomicAdd(&wc[0], ncell);
+            __builtin_amdgcn_wave_barrier();
+            if (first) {
+                const uint32_t N = wc[0];
+                prof[10] += N ? 1 : 0;
+                prof[4] += (N + 63) / 64;
+            }
         }
         if (PROF) tb = stamp();
-        if (SKIP && !occupied && nearest == kInf && s.neg < 8u) {
-            bool exited;
-            BRICK_SKIP4(s, gk, exited);
-            if (exited) break;
-            occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
-            continue;
-        }
         bool crossed;
         float t_exit;
         DDA_STEP(s, gk, sh, crossed, t_exit);
         if (nearest <= t_exit) break;                      // stage3.zig:179-182
         if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
         if (PROF) { const uint64_t tc = stamp(); prof[0] += tb - ta; prof[1] += tc - tb; }
+    }
+    return nearest;
+}
+
+// Scene.traceRay for the 64 rays of a wave, walked in lockstep, with the
+// triangle tests of each step shared across the wave.
+//
+// Per-lane testing (trace_ray) runs a wave's triangle loop as long as its
+// busiest lane: on the contest scene a wave trip that tests anything tests
+// 26 (ref, ray) pairs on average, yet costs 3 two-triangle trips (the max
+// over lanes), i.e. ~7% of the lanes do useful work.  Here, each step:
+//  1. every walking lane loads its cell's range [b, b+n) (if its brick is
+//     occupied);
+//  2. the wave lays all pairs (owner lane, ref) out in lane order - owner i
+//     covers pair slots [off_i, off_i + n_i) - and tests them 64 at a time,
+//     lane q taking pair slot r + q (one MT test per lane per round);
+//  3. each owner's winner is the lexicographic min of (t, ref index) over its
+//     pairs with 0 < t < nearest (an LDS 64-bit atomicMin on t's bits: t > 0
+//     orders like its bit pattern), which is exactly the first ref of the
+//     cell (stage3.zig:164-178 order) reaching the smallest accepted t, i.e.
+//     what the sequential `nearest > t && t > 0` loop keeps; the winner's
+//     lane also leaves (u, v) in LDS;
+//  4. every walking lane steps its DDA and applies the break (stage3.zig:179).
+// All lanes of the wave execute the loop (lanes without a ray pass alive =
+// false), so the cross-lane steps run converged.  LDS per wave: the rays
+// (o, nearest before the step | d, ref base) and the (key, u, v) slots.
+struct WaveLds {
+    float4 ray[128];               // [2*lane]: o.xyz, nearest0; [2*lane+1]: d.xyz, unused
+    unsigned long long best[64];   // per owner: (t bits << 32) | ref
+    float2 uv[64];
+    uint32_t base[64];             // per owner: ref of pair slot 0 (b - off, mod 2^32)
+};
+
+__device__ __forceinline__ float trace_wave(const TraceParams& p, const uint32_t* occ, WaveLds& L, bool alive,
+                                            v3 o, v3 d, float& hu, float& hv, uint32_t& hidx) {
+    const uint32_t lane = threadIdx.x & 63u;
+    float nearest = kInf;
+    hu = hv = 0.0f;
+    hidx = 0;
+    Dda s;
+    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
+    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
+    bool active = alive && dda_setup(p, o, d, s);
+    const uint32_t sh = p.occ_shift;
+    const GridK gk = grid_consts(p);
+    bool occupied = active && brick_occupied(p, occ, s.c0, s.c1, s.c2);
+    while (__ballot(active) != 0ull) {
+        uint32_t b = 0, n = 0;
+        if (active && occupied) {
+            const uint2 cell = p.cells[s.lin];
+            b = cell.x;
+            n = cell.y - cell.x;
+        }
+        const uint64_t own = __ballot(n != 0u);
+        if (own != 0ull) {
+            uint32_t my_off = 0, N = 0;
+            for (uint64_t m = own; m != 0ull; m &= m - 1ull) {      // scalar: owners in lane order
+                const uint32_t i = (uint32_t)__builtin_ctzll(m);
+                if (lane == i) my_off = N;
+                N += (uint32_t)__builtin_amdgcn_readlane((int)n, (int)i);
+            }
+            L.ray[2 * lane] = make_float4(o.x, o.y, o.z, nearest);
+            L.ray[2 * lane + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+            L.base[lane] = b - my_off;
+            L.best[lane] = ~0ull;
+            __builtin_amdgcn_wave_barrier();
+            // workers: the lanes the compiler keeps enabled here (it may mask
+            // lanes whose walk has ended), numbered densely
+            const uint64_t ex = __ballot(1);
+            const uint32_t W = (uint32_t)__popcll(ex);
+            const uint32_t wi = (uint32_t)__popcll(ex & (lane ? (~0ull >> (64u - lane)) : 0ull));
+            for (uint32_t r = 0; r < N; r += W) {
+                const uint32_t q = r + wi;
+                uint32_t owner = 0, acc = 0;
+                for (uint64_t m = own; m != 0ull; m &= m - 1ull) {
+                    const uint32_t i = (uint32_t)__builtin_ctzll(m);
+                    const uint32_t ni = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)i);
+                    if (acc + ni > r && acc < r + W) owner = (q >= acc && q < acc + ni) ? i : owner;
+                    acc += ni;
+                }
+                const bool valid = q < N;
+                const float4 ra = L.ray[2 * owner], rb = L.ray[2 * owner + 1];
+                const uint32_t j = L.base[owner] + q;
+                bool cand = false;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                if (valid) {
+                    const float4 A = p.tri_pos[3 * j + 0], B = p.tri_pos[3 * j + 1], C = p.tri_pos[3 * j + 2];
+                    cand = tri_ray(mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z), mk(ra.x, ra.y, ra.z),
+                                   mk(rb.x, rb.y, rb.z), &t, &u, &v) &&
+                           ra.w > t && t > 0.0f;
+                }
+                const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
+                if (cand) atomicMin(&L.best[owner], key);
+                __builtin_amdgcn_wave_barrier();
+                if (cand && L.best[owner] == key) L.uv[owner] = make_float2(u, v);
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (n != 0u) {
+                const unsigned long long k = L.best[lane];
+                if (k != ~0ull) {
+                    nearest = __uint_as_float((uint32_t)(k >> 32));
+                    hidx = (uint32_t)k;
+                    const float2 uv = L.uv[lane];
+                    hu = uv.x;
+                    hv = uv.y;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (active) {
+            bool crossed;
+            float t_exit;
+            DDA_STEP(s, gk, sh, crossed, t_exit);
+            if (nearest <= t_exit) active = false;                 // stage3.zig:179-182
+            else if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
+        }
     }
     return nearest;
 }
@@ -243,7 +397,9 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
     // cell+tris, dda, trace, shade, fetch, total (PROF); cell loads, non-empty cells (STATS)
     // + wave trips of the cell loop / triangle-batch loop (STATS)
-    uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // [10]: trips with any test (STATS; was mailbox counts), [4]: shared rounds (STATS)
+    uint64_t prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __shared__ uint32_t s_wcnt[2 * (kTraceBlock / 64)];
     const uint64_t t_begin = PROF ? stamp() : 0;
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
@@ -287,7 +443,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
             float hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
             const uint64_t t_tr = PROF ? stamp() : 0;
-            const float t = trace_ray<STATS, PROF, TB>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof);
+            const float t = trace_ray<STATS, PROF, TB>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof,
+                                                       s_wcnt);
             const uint64_t t_sh = PROF ? stamp() : 0;
             if (PROF) prof[2] += t_sh - t_tr;
             if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
@@ -330,8 +487,12 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TracePar
     if (STATS) {
         s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits);
         s4 = wave_sum(prof[6]); s5 = wave_sum(prof[7]);
-        const unsigned long long s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]);
-        if (lane == 0) { atomicAdd(&p.stats[6], s6); atomicAdd(&p.stats[7], s7); }
+        const unsigned long long s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]), s8 = wave_sum(prof[10]);
+        const unsigned long long s9 = wave_sum(prof[4]);
+        if (lane == 0) {
+            atomicAdd(&p.stats[6], s6); atomicAdd(&p.stats[7], s7); atomicAdd(&p.stats[14], s8);
+            atomicAdd(&p.stats[15], s9);
+        }
     }
     if (lane == 0) {
         atomicAdd(&p.stats[0], s0);
@@ -452,7 +613,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
     }
 }
 
-template <int TB, int MINW, bool PRIMARY, bool SKIP = false>
+template <int TB, int MINW, bool PRIMARY, bool MB = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -466,7 +627,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
     const uint32_t n = PRIMARY ? p.total : *w.n_in;
     uint32_t n_seg = 0, dummy = 0;
-    uint64_t prof_dummy[10];
+    uint64_t prof_dummy[11];
 
     for (;;) {
         uint32_t base = 0;
@@ -503,14 +664,78 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
                 ++n_seg;
                 float hu = 0.0f, hv = 0.0f;
                 uint32_t hidx = 0;
-                const float t = trace_ray<false, false, TB, SKIP>(p, s_occ, o, d, hu, hv, hidx, dummy,
-                                                                  dummy, prof_dummy);
+                const float t = trace_ray<false, false, TB, MB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy,
+                                                                prof_dummy);
                 cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
             }
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
         }
         wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask);
+    }
+    const unsigned long long s0 = wave_sum(n_seg);
+    if (lane == 0) atomicAdd(&p.stats[0], s0);
+}
+
+// wf_kernel with the wave-cooperative traversal (trace_wave).  Dynamic LDS:
+// the occupancy bits, then one WaveLds per wave.
+template <int MINW, bool PRIMARY>
+__global__ __launch_bounds__(kTraceBlock, MINW) void wf_wave_kernel(const WfParams w) {
+    const TraceParams& p = w.t;
+    __shared__ double s_zig[514];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
+    __syncthreads();
+    WaveLds& L = reinterpret_cast<WaveLds*>(s_occ + ((p.occ_words + 3u) & ~3u))[threadIdx.x >> 6];
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t n = PRIMARY ? p.total : *w.n_in;
+    uint32_t n_seg = 0;
+
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(w.fetch, 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= n) break;
+        const uint32_t i = base + lane;
+        const bool valid = i < n;
+        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
+        Rng rng;
+        rng.s = 0;
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 1);
+        if (valid) {
+            if (PRIMARY) {
+                item = i;
+                camera_ray(p, item, rng, o, d);
+                depth = p.max_bounce;
+            } else {
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                o = mk(a.x, a.y, a.z);
+                item = __float_as_uint(a.w);
+                d = mk(b.x, b.y, b.z);
+                depth = __float_as_uint(b.w) & 0xFFFFu;
+                slot = __float_as_uint(b.w) >> 16;
+                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+                mask = __float_as_uint(c.z);
+            }
+        }
+        const bool alive = valid && depth != 0u;
+        float hu, hv;
+        uint32_t hidx;
+        const float t = trace_wave(p, s_occ, L, alive, o, d, hu, hv, hidx);
+        bool cont = false;
+        if (valid) {
+            v3 Lr = mk(0, 0, 0);
+            if (alive) {
+                ++n_seg;
+                cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, Lr);
+            }
+            if (!cont) w.term[item] = make_float4(Lr.x, Lr.y, Lr.z, __uint_as_float(mask));
+        }
+        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -546,6 +771,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfPar
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     Dda s;
+    Mailbox mbx;
+    mbx.reset();
     s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
     s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
     for (;;) {
@@ -571,6 +798,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfPar
                     nearest = kInf;
                     hu = hv = 0.0f;
                     hidx = 0;
+                    mbx.reset();
                     if (dda_setup(p, o, d, s)) {                   // stage3.zig:153-156
                         active = true;
                         occupied = brick_occupied(p, s_occ, s.c0, s.c1, s.c2);
@@ -588,7 +816,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfPar
             if (occupied) {
                 const uint2 cell = p.cells[s.lin];
                 uint32_t nt = 0;
-                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, nt);
+                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, nt, nullptr, mbx);
             }
             bool crossed;
             float t_exit;
@@ -857,6 +1085,29 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     delete c;
 }
 
+// Shape id per ref for the mailbox: refs with bit-identical (v0, e1, e2)
+// share an id (the bake's per-cell copies of one triangle, and any
+// coincident triangles, whose tests are identical too).
+static std::vector<uint32_t> shape_ids(const float* pos, uint32_t n) {
+    struct Key { uint32_t w[9]; bool operator==(const Key& o) const { return !memcmp(w, o.w, sizeof w); } };
+    struct Hash {
+        size_t operator()(const Key& k) const {
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            for (uint32_t x : k.w) h = (h ^ x) * 0xBF58476D1CE4E5B9ull, h ^= h >> 29;
+            return (size_t)h;
+        }
+    };
+    std::unordered_map<Key, uint32_t, Hash> ids;
+    ids.reserve(n);
+    std::vector<uint32_t> out(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        Key k;
+        memcpy(k.w, pos + 9ull * i, sizeof k.w);
+        out[i] = ids.emplace(k, (uint32_t)ids.size()).first->second;
+    }
+    return out;
+}
+
 static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&c->ev_begin));
@@ -872,9 +1123,12 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
     std::vector<float4> pos(3 * nr), dat(4 * nr);
+    const std::vector<uint32_t> shape = shape_ids(s->triangles_pos, c->nrefs);
     for (uint32_t i = 0; i < c->nrefs; ++i) {
         const float* q = s->triangles_pos + 9ull * i;
-        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], 0.0f);
+        float idf;
+        memcpy(&idf, &shape[i], 4);
+        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], idf);
         pos[3 * i + 1] = make_float4(q[3], q[4], q[5], 0.0f);
         pos[3 * i + 2] = make_float4(q[6], q[7], q[8], 0.0f);
         float tmp[16];
@@ -1058,8 +1312,11 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
 
     // occupancy-sized persistent grids
-    const size_t lds_bytes = 4ull * c->occ_words;
     const int tblock = trace_block();
+    const char* wave_env = getenv("ZRT_WAVE");
+    const bool wave_mode = wf && !split && wave_env && atoi(wave_env) == 1;
+    const size_t lds_bytes = wave_mode ? 16ull * ((c->occ_words + 3u) / 4u) + (size_t)(tblock / 64) * sizeof(WaveLds)
+                                       : 4ull * c->occ_words;
     auto grid_for = [&](const void* f, uint32_t* blocks) -> int {
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
@@ -1086,10 +1343,14 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         case 7: ZRT_WF_PICK(K, 7); break;                                    \
         default: ZRT_WF_PICK(K, 8); break;                                   \
     }
-        const char* sk = getenv("ZRT_SKIP");
-        if (split) {
+        const char* mbe = getenv("ZRT_MB");
+        if (wave_mode) {
+            if (mw == 5) { wf_first = (WfFn)wf_wave_kernel<5, true>; wf_next = (WfFn)wf_wave_kernel<5, false>; }
+            else if (mw == 8) { wf_first = (WfFn)wf_wave_kernel<8, true>; wf_next = (WfFn)wf_wave_kernel<8, false>; }
+            else { wf_first = (WfFn)wf_wave_kernel<6, true>; wf_next = (WfFn)wf_wave_kernel<6, false>; }
+        } else if (split) {
             ZRT_WF_SWITCH(wf_trace_kernel)
-        } else if (c->occ_shift == 2 && sk && atoi(sk) == 1) {
+        } else if (mbe && atoi(mbe) == 1) {
             if (mw == 5) { wf_first = (WfFn)wf_kernel<kTriBatch, 5, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 5, false, true>; }
             else { wf_first = (WfFn)wf_kernel<kTriBatch, 6, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 6, false, true>; }
         } else {
@@ -1219,8 +1480,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 hs[8], hs[9], hs[10], hs[11], hs[12], hs[13]);
     if (getenv("ZRT_CELL_STATS") && want_stats)
         fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu, "
-                "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu}}\n",
-                hs[1], hs[4], hs[5], hs[2], hs[6], hs[7]);
+                "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu, \"trips_with_tests\": %llu, \"shared_rounds\": %llu}}\n",
+                hs[1], hs[4], hs[5], hs[2], hs[6], hs[7], hs[14], hs[15]);
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
