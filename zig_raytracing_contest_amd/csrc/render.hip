@@ -535,7 +535,43 @@ struct WfParams {
     float4* hit;              // split mode: [queue index] (t, u, v, tri) of this bounce
     uint32_t T;               // items in this pass
     uint32_t refill;          // split mode: idle lanes before a wave fetches rays
+    uint32_t* hist;           // ray sort: per-key counts of the appended paths (null: no sort)
+    uint32_t sort_bits;       // ray sort: origin-region bits per axis
 };
+
+// Ray-sort key of a continuing path: the origin's region in a 2^R per axis
+// subdivision of the grid bbox (Morton order), then the direction octant.
+// Paths of one key start close together heading the same way, so a wave of
+// them walks overlapping cells and tests the same triangles (coalesced
+// loads, similar walk lengths).
+__device__ __forceinline__ uint32_t sort_key(const TraceParams& p, v3 o, v3 d, uint32_t R) {
+    const float n = (float)(1u << R);
+    uint32_t r[3];
+    const float oc[3] = {o.x, o.y, o.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float f = (oc[a] - p.bmin[a]) / (p.bmax[a] - p.bmin[a]) * n;
+        r[a] = f > 0.0f ? min((uint32_t)f, (1u << R) - 1u) : 0u;   // NaN -> 0
+    }
+    uint32_t m = 0;
+    for (uint32_t b = 0; b < R; ++b)
+        m |= (((r[0] >> b) & 1u) << (3 * b)) | (((r[1] >> b) & 1u) << (3 * b + 1)) |
+             (((r[2] >> b) & 1u) << (3 * b + 2));
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    return (m << 3) | oct;
+}
+
+// Count one key per lane of `live` into hist, one atomic per distinct key
+// of the wave.
+__device__ __forceinline__ void wave_key_count(uint32_t* hist, bool live, uint32_t key) {
+    uint64_t pend = __ballot(live);
+    while (pend) {
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(pend));
+        const uint64_t m = __ballot(live && key == k);
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(pend)) atomicAdd(&hist[k], (uint32_t)__popcll(m));
+        pend &= ~m;
+    }
+}
 
 // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35) for
 // pass item `item` (= s_local * P + packed pixel); leaves rng after the jitter.
@@ -600,6 +636,11 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
                                          uint32_t mask) {
     const uint64_t bal = __ballot(cont);
     if (!bal) return;
+    uint32_t key = 0;
+    if (w.hist) {
+        key = cont ? sort_key(w.t, o, d, w.sort_bits) : 0u;
+        wave_key_count(w.hist, cont, key);
+    }
     uint32_t ob = 0;
     if ((threadIdx.x & 63u) == 0) ob = atomicAdd(w.n_out, (uint32_t)__popcll(bal));
     ob = __builtin_amdgcn_readfirstlane(ob);
@@ -609,7 +650,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
         w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
         w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s),
                                               __uint_as_float((uint32_t)(rng.s >> 32)),
-                                              __uint_as_float(mask), 0.0f);
+                                              __uint_as_float(mask), __uint_as_float(key));
     }
 }
 
@@ -882,6 +923,61 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(const WfParams w) {
     if (lane == 0) atomicAdd(&p.stats[0], s0);
 }
 
+// Ray sort between bounces (counting sort on sort_key): exclusive scan of
+// the key counts into cursors (one block), then every record moves to its
+// key's range (one returning atomic per distinct key per wave).  The order
+// inside a key is arrival order; results do not depend on queue order (every
+// path writes only its own item's slots).
+__global__ __launch_bounds__(1024) void sort_scan_kernel(uint32_t* hist, uint32_t* cursor, uint32_t nbins) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nbins + 1023u) / 1024u;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < min(b0 + per, nbins); ++b) sum += hist[b];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {            // inclusive Hillis-Steele scan
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t b = b0; b < min(b0 + per, nbins); ++b) {
+        cursor[b] = run;
+        run += hist[b];
+        hist[b] = 0;                                           // clean for the next bounce
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const float4* __restrict__ src, float4* dst,
+                                                              const uint32_t* n_in, uint32_t* cursor) {
+    const uint32_t n = *n_in;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * 64u; base < n; base += nwaves * 64u) {
+        const uint32_t i = base + lane;
+        const bool live = i < n;
+        float4 a = make_float4(0, 0, 0, 0), b = a, c = a;
+        if (live) { a = src[3ull * i]; b = src[3ull * i + 1]; c = src[3ull * i + 2]; }
+        const uint32_t key = __float_as_uint(c.w);
+        uint64_t pend = __ballot(live);
+        uint32_t pos = 0;
+        while (pend) {
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(pend));
+            const uint64_t m = __ballot(live && key == k);
+            uint32_t ob = 0;
+            if (lane == (uint32_t)__builtin_ctzll(pend)) ob = atomicAdd(&cursor[k], (uint32_t)__popcll(m));
+            ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)__builtin_ctzll(pend));
+            if ((m >> lane) & 1ull) pos = ob + (uint32_t)__popcll(m & below);
+            pend &= ~m;
+        }
+        if (live) { dst[3ull * pos] = a; dst[3ull * pos + 1] = b; dst[3ull * pos + 2] = c; }
+    }
+}
+
 // Fold + ordered sample sum + toRGB for wavefront mode (stage3.zig:219,
 // :236-242): per sample, L = terminal radiance, then e + a*L for every slot
 // that scattered, from the last bounce back to the first.
@@ -1022,6 +1118,8 @@ struct zrt_context {
     float4* d_term = nullptr; size_t term_cap = 0;
     float4* d_stk = nullptr; size_t stk_cap = 0;
     float4* d_hit = nullptr; size_t hit_cap = 0;
+    uint32_t* d_hist = nullptr; size_t hist_cap = 0;     // ray sort
+    uint32_t* d_cursor = nullptr; size_t cursor_cap = 0;
     uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
@@ -1075,7 +1173,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
-                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_hit, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
+                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_hit, c->d_hist, c->d_cursor, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -1344,7 +1442,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         default: ZRT_WF_PICK(K, 8); break;                                   \
     }
         const char* mbe = getenv("ZRT_MB");
-        if (wave_mode) {
+        const char* tbe = getenv("ZRT_TB");      // tuning sweeps only
+        const int tbv = tbe ? atoi(tbe) : kTriBatch;
+        if (!wave_mode && !split && tbv != kTriBatch && (tbv == 1 || tbv == 3 || tbv == 4)) {
+            if (tbv == 1) { wf_first = (WfFn)wf_kernel<1, 6, true>; wf_next = (WfFn)wf_kernel<1, 6, false>; }
+            if (tbv == 3) { wf_first = (WfFn)wf_kernel<3, 6, true>; wf_next = (WfFn)wf_kernel<3, 6, false>; }
+            if (tbv == 4) { wf_first = (WfFn)wf_kernel<4, 6, true>; wf_next = (WfFn)wf_kernel<4, 6, false>; }
+        } else if (wave_mode) {
             if (mw == 5) { wf_first = (WfFn)wf_wave_kernel<5, true>; wf_next = (WfFn)wf_wave_kernel<5, false>; }
             else if (mw == 8) { wf_first = (WfFn)wf_wave_kernel<8, true>; wf_next = (WfFn)wf_wave_kernel<8, false>; }
             else { wf_first = (WfFn)wf_wave_kernel<6, true>; wf_next = (WfFn)wf_wave_kernel<6, false>; }
@@ -1367,6 +1471,15 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         return rc;
     }
     uint32_t refill = 48;
+    // ray sort between bounces (ZRT_SORT = origin-region bits per axis, 0 = off)
+    uint32_t sort_bits = 0;
+    if (const char* e = getenv("ZRT_SORT")) sort_bits = (uint32_t)std::max(0, std::min(4, atoi(e)));
+    const bool sorting = wf && sort_bits > 0 && mb > 1;
+    const uint32_t nbins = 8u << (3 * sort_bits);
+    if (sorting) {
+        if ((rc = grow(&c->d_hist, &c->hist_cap, nbins)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_cursor, &c->cursor_cap, nbins)) != ZRT_OK) return rc;
+    }
     if (const char* e = getenv("ZRT_REFILL")) refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
     const uint32_t shade_blocks = (uint32_t)c->num_cus * 8u;
 
@@ -1425,10 +1538,19 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.hit = c->d_hit;
             W.T = (uint32_t)T;
             W.refill = refill;
+            W.sort_bits = sort_bits;
             const uint32_t nb = std::max<uint32_t>(mb, 1);
+            if (sorting) HIP_TRY(hipMemsetAsync(c->d_hist, 0, 4ull * nbins, c->stream));
             for (uint32_t k = 0; k < nb; ++k) {
-                W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
-                W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
+                if (sorting) {             // appended to q0, sorted into q1 for the next bounce
+                    W.q_in = c->d_q1;
+                    W.q_out = c->d_q0;
+                } else {
+                    W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
+                    W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
+                }
+                const bool sort_out = sorting && k + 1 < nb;
+                W.hist = sort_out ? c->d_hist : nullptr;
                 W.n_in = n + k;
                 W.n_out = n + k + 1;
                 W.fetch = fetch + k;
@@ -1447,6 +1569,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                         hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
                     else
                         hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
+                    HIP_TRY(hipGetLastError());
+                }
+                if (sort_out) {
+                    hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_hist, c->d_cursor,
+                                       nbins);
+                    hipLaunchKernelGGL(sort_scatter_kernel, dim3(shade_blocks), dim3(kBlock), 0, c->stream,
+                                       (const float4*)c->d_q0, c->d_q1, (const uint32_t*)(n + k + 1), c->d_cursor);
                     HIP_TRY(hipGetLastError());
                 }
             }
@@ -1485,10 +1614,19 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
+    const bool wf_debug = getenv("ZRT_WF_DEBUG") != nullptr;
     for (uint32_t e = 0; e + 1 < ne; e += 2) {   // trace launches only (not shade / resolve)
         float t = 0.0f;
         HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[e], c->ev_trace[e + 1]));
         st.trace_kernel_ms += t;
+        if (wf_debug) fprintf(stderr, "{\"zrt_launch\": %u, \"ms\": %.3f}\n", e / 2, t);
+    }
+    if (wf_debug && wf) {   // live paths entering each bounce of the last pass
+        std::vector<uint32_t> nk(mb + 2, 0);
+        HIP_TRY(hipMemcpy(nk.data(), c->d_wfc, 4ull * (mb + 2), hipMemcpyDeviceToHost));
+        fprintf(stderr, "{\"zrt_last_pass_items\": %llu, \"live\": [", (unsigned long long)T);
+        for (uint32_t k = 1; k <= mb; ++k) fprintf(stderr, "%s%u", k > 1 ? ", " : "", nk[k]);
+        fprintf(stderr, "]}\n");
     }
     st.trace_launches = launches;
     st.segments = hs[0];
