@@ -24,40 +24,27 @@ struct TestGrid {
     }
 };
 
-// bmax: fmaxf of the exit t of every cell passed since the previous record
-// (what the park kernel folds into B; +inf at the grid exit)
 struct Rec {
     uint32_t c0, c1, c2, lin;
-    float tn0, tn1, tn2, bmax;
+    float tn0, tn1, tn2;
     bool operator==(const Rec& o) const {
         return c0 == o.c0 && c1 == o.c1 && c2 == o.c2 && lin == o.lin &&
-               !memcmp(&tn0, &o.tn0, 4) && !memcmp(&tn1, &o.tn1, 4) && !memcmp(&tn2, &o.tn2, 4) &&
-               !memcmp(&bmax, &o.bmax, 4);
+               !memcmp(&tn0, &o.tn0, 4) && !memcmp(&tn1, &o.tn1, 4) && !memcmp(&tn2, &o.tn2, 4);
     }
 };
 
-static Rec rec(const Dda& s, float& acc) {
-    Rec r{s.c0, s.c1, s.c2, s.lin, s.tn0, s.tn1, s.tn2, acc};
-    acc = -kInf;
-    return r;
-}
-static Rec exit_rec(float& acc) {
-    acc = fmaxf(acc, kInf);
-    return Rec{~1u, ~1u, ~1u, ~1u, 0, 0, 0, acc};
-}
+static Rec rec(const Dda& s) { return Rec{s.c0, s.c1, s.c2, s.lin, s.tn0, s.tn1, s.tn2}; }
 
 // reference: every cell; keep the ones in occupied bricks
 static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
     std::vector<Rec> out;
-    float acc = -kInf;
     for (int guard = 0; guard < 100000; ++guard) {
-        if (g.occupied(s.c0, s.c1, s.c2)) out.push_back(rec(s, acc));
+        if (g.occupied(s.c0, s.c1, s.c2)) out.push_back(rec(s));
         bool crossed;
         float t_exit;
         DDA_STEP(s, k, 2, crossed, t_exit);
         (void)crossed;
-        acc = fmaxf(acc, t_exit);
-        if (t_exit == kInf) { out.push_back(exit_rec(acc)); return out; }
+        if (t_exit == kInf) return out;
     }
     out.push_back(Rec{~0u, ~0u, ~0u, ~0u, 0, 0, 0});
     return out;
@@ -66,53 +53,21 @@ static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
 // product: skip unoccupied bricks whole
 static std::vector<Rec> walk_skip(const TestGrid& g, const GridK& k, Dda s, uint64_t* skips) {
     std::vector<Rec> out;
-    float acc = -kInf;
     for (int guard = 0; guard < 100000; ++guard) {
         const bool occ = g.occupied(s.c0, s.c1, s.c2);
         if (!occ && s.neg < 8u) {
             bool exited;
-            float ex;
-            BRICK_SKIP4(s, k, exited, ex);
+            BRICK_SKIP4(s, k, exited);
             ++*skips;
-            if (exited) { out.push_back(exit_rec(acc)); return out; }
-            acc = fmaxf(acc, ex);
+            if (exited) return out;
             continue;
         }
-        if (occ) out.push_back(rec(s, acc));
+        if (occ) out.push_back(rec(s));
         bool crossed;
         float t_exit;
         DDA_STEP(s, k, 2, crossed, t_exit);
         (void)crossed;
-        acc = fmaxf(acc, t_exit);
-        if (t_exit == kInf) { out.push_back(exit_rec(acc)); return out; }
-    }
-    out.push_back(Rec{~0u, ~0u, ~0u, ~0u, 0, 0, 0});
-    return out;
-}
-
-// product (park kernel): DDA_ADVANCE over the brick when it is empty, over
-// the cell otherwise
-static std::vector<Rec> walk_adv(const TestGrid& g, const GridK& k, Dda s, uint64_t* skips, uint64_t* bad_step) {
-    std::vector<Rec> out;
-    float acc = -kInf;
-    for (int guard = 0; guard < 100000; ++guard) {
-        const bool occ = g.occupied(s.c0, s.c1, s.c2);
-        const bool br = !occ && s.neg < 8u;
-        if (occ) out.push_back(rec(s, acc));
-        Dda ref = s;
-        bool rc = false;
-        float rt = 0.0f;
-        if (!br) DDA_STEP(ref, k, 2, rc, rt);
-        bool crossed, exited;
-        float t_exit;
-        DDA_ADVANCE(s, k, br, crossed, exited, t_exit);
-        *skips += br ? 1 : 0;
-        if (!br && !exited) {   // a cell advance is exactly Iterator.next
-            if (!(rec(ref, acc) == rec(s, acc)) || rc != crossed || memcmp(&rt, &t_exit, 4)) ++*bad_step;
-        }
-        if (!br && exited && rt != kInf) ++*bad_step;
-        acc = fmaxf(acc, t_exit);
-        if (t_exit == kInf) { out.push_back(exit_rec(acc)); return out; }
+        if (t_exit == kInf) return out;
     }
     out.push_back(Rec{~0u, ~0u, ~0u, ~0u, 0, 0, 0});
     return out;
@@ -123,7 +78,7 @@ int main(int argc, char** argv) {
     const int n_rays = argc > 2 ? atoi(argv[2]) : 4000;
     std::mt19937_64 rng(12345);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
-    uint64_t total = 0, skips = 0, ties = 0, fails = 0, adv_skips = 0, bad_step = 0;
+    uint64_t total = 0, skips = 0, ties = 0, fails = 0;
     for (int gi = 0; gi < n_grids; ++gi) {
         TestGrid g;
         const bool pow2 = gi % 3 == 0;     // exact arithmetic -> many crossing ties
@@ -167,11 +122,6 @@ int main(int argc, char** argv) {
             if (s.tn0 == s.tn1 || s.tn1 == s.tn2 || s.tn0 == s.tn2) ++ties;
             const auto a = walk_cells(g, k, s);
             const auto b = walk_skip(g, k, s, &skips);
-            const auto w = walk_adv(g, k, s, &adv_skips, &bad_step);
-            if (!(a.size() == w.size() && std::equal(a.begin(), a.end(), w.begin()))) {
-                if (++fails <= 5)
-                    fprintf(stderr, "ADVANCE MISMATCH grid %d ray %d: %zu vs %zu cells\n", gi, r, a.size(), w.size());
-            }
             if (!(a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin()))) {
                 if (++fails <= 5)
                     fprintf(stderr, "MISMATCH grid %d ray %d: %zu vs %zu cells (o=%g,%g,%g d=%g,%g,%g)\n", gi, r,
@@ -179,9 +129,8 @@ int main(int argc, char** argv) {
             }
         }
     }
-    printf("{\"rays\": %llu, \"skips\": %llu, \"adv_skips\": %llu, \"tie_starts\": %llu, \"bad_steps\": %llu, "
-           "\"fails\": %llu}\n",
-           (unsigned long long)total, (unsigned long long)skips, (unsigned long long)adv_skips,
-           (unsigned long long)ties, (unsigned long long)bad_step, (unsigned long long)fails);
-    return fails || bad_step ? 1 : 0;
+    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"fails\": %llu}\n",
+           (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
+           (unsigned long long)fails);
+    return fails ? 1 : 0;
 }

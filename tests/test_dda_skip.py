@@ -23,18 +23,3 @@ def test_brick_skip_matches_cell_walk(tmp_path):
     r = subprocess.run([str(exe), "60", "6000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert '"fails": 0' in r.stdout
-
-
-@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
-def test_flat_triangle_test_matches_tri_ray(tmp_path):
-    """tri_ray_flat (park kernel test rounds) vs tri_ray: same accepts, same
-    t/u/v bits (tests/cpp/tri_flat_check.cpp)."""
-    exe = tmp_path / "trichk"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
-                    "-I", os.path.join(ROOT, "zig_raytracing_contest_amd", "csrc"),
-                    "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "tri_flat_check.cpp"), "-o", str(exe)],
-                   check=True)
-    r = subprocess.run([str(exe), "1000000"], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr + r.stdout
-    assert '"fails": 0' in r.stdout

@@ -183,40 +183,11 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
         tuple(int(x) for x in ctr[:4])
 
 
-# Timed-path kernels (no counting build) against the oracle on every scene.
-# park: the walk / park / test schedule at its extremes (test a lane as soon
-# as it parks, or only when the whole wave has parked; refill per lane or per
-# wave) must not change a single bit.
-MODES = [("wf", {}), ("park", {}), ("park", {"ZRT_TEST_MIN": "1", "ZRT_REFILL": "1"}),
-         ("park", {"ZRT_TEST_MIN": "64", "ZRT_REFILL": "64"}), ("split", {})]
-
-
-@pytest.mark.parametrize("mode,env", MODES, ids=lambda m: str(m))
-@pytest.mark.parametrize("name,camname,w,h,spp", CASES)
-def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mode, env, name, camname,
-                                         w, h, spp):
-    monkeypatch.setenv("ZRT_MODE", mode)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    soup = scenes.get_scene(name)
-    c = soup.camera(camname)
-    aspect = c.aspect
-    cam = camera_for(soup, camname, None if aspect else w, h)
-    img, res = gpu_scenes(name).render(cam, num_samples=spp, max_bounce=4, linear=True)
-    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, aspect, None if aspect else w, h)
-    rgb, lin, ctr = oracle_mod.OracleScene(soup).render(ocam, spp, 4, oracle_mod.RNG_PATH, 0, 16)
-    pix = native.tile_pixels(cam.w, cam.h)
-    assert np.array_equal(res["linear"], lin[pix])
-    assert np.array_equal(img.reshape(-1, 3), rgb)
-    assert res["stats"]["segments"] == int(ctr[0])
-
-
 # per-item pass bytes of each kernel organisation (render.hip: per_item)
-PER_ITEM = {"mega": 16, "wf": 96 + 16 + 32 * 4, "split": 96 + 16 + 16 + 32 * 4,
-            "park": 96 + 16 + 32 * 4}
+PER_ITEM = {"mega": 16, "wf": 96 + 16 + 32 * 4, "split": 96 + 16 + 16 + 32 * 4}
 
 
-@pytest.mark.parametrize("mode", ["wf", "split", "mega", "park"])
+@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
 def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
     """Pass splits (sample ranges), rank splits (tile sets) and the three kernel
     organisations (fused wavefront / split wavefront / megakernel) all give the
@@ -241,7 +212,7 @@ def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
     assert np.array_equal(ref, img)
 
 
-@pytest.mark.parametrize("mode", ["wf", "split", "mega", "park"])
+@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
 @pytest.mark.parametrize("mb", [0, 1, 5, 9, 17])
 def test_render_max_bounce_variants(oracle_mod, gpu_scenes, monkeypatch, mode, mb):
     monkeypatch.setenv("ZRT_MODE", mode)

@@ -6,7 +6,7 @@ tag=${1:-r01}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q > $out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > $out/bench.json 2> $out/bench.err

@@ -103,13 +103,10 @@ struct GridK {
 // merge of the three sequences ordered by (t, -axis).  The brick is left by
 // the first, in that order, of the brick-exit crossings E_a = T_a(m_a)
 // (m_a = cells to the brick face along a), and every other axis b has then
-// taken exactly the crossings T_b(j), j < m_b, that precede it.  Not used
-// with a -inf/NaN sequence (neg bit 3).
-// EXITED: the skip left the grid (Iterator.next returned +inf).
-// T_EXIT: the crossing that leaves the brick = the largest exit t of the
-// cells passed (the merge is nondecreasing), i.e. the last t_exit traceRay's
-// break test would have compared nearest against.  So the skip is exact for
-// any nearest: the walk ends inside the brick iff nearest <= T_EXIT.
+// taken exactly the crossings T_b(j), j < m_b, that precede it.  Only used
+// while nothing is hit yet (nearest = inf: no cell of an empty brick can end
+// the walk except the grid exit) and with no -inf/NaN sequence (neg bit 3).
+// EXITED: the skip left the grid (traceRay returns no hit).
 #define SKIP_AXIS(S, G, A)                                                                    \
     const bool n##A##_ = ((S).neg >> A) & 1u;                                                 \
     const uint32_t lo##A##_ = (S).c##A & ~3u;                                                 \
@@ -132,7 +129,7 @@ struct GridK {
               : (k##A##_ == 1u ? T##A##2_                                                     \
               : (k##A##_ == 2u ? T##A##3_ : (k##A##_ == 3u ? T##A##4_ : T##A##4_ + (S).td##A))); \
     (S).c##A = n##A##_ ? (S).c##A - k##A##_ : (S).c##A + k##A##_;
-#define BRICK_SKIP4(S, G, EXITED, T_EXIT)                                                            \
+#define BRICK_SKIP4(S, G, EXITED)                                                             \
     do {                                                                                      \
         SKIP_AXIS(S, G, 0)                                                                    \
         SKIP_AXIS(S, G, 1)                                                                    \
@@ -145,60 +142,6 @@ struct GridK {
         SKIP_COUNT(S, 1, x0_)                                                                 \
         SKIP_COUNT(S, 2, !x2_)                                                                \
         (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                       \
-        (T_EXIT) = ex_;                                                                       \
-        (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
-    } while (0)
-
-
-// One advance of the walk, branch-free over a per-lane region: BRICK = false
-// is exactly one Iterator.next (the region is the current cell: m_a = 1, the
-// exit axis is DDA_STEP's argmin with the same tie booleans, T_EXIT is its
-// crossing or +inf at the grid exit); BRICK = true is BRICK_SKIP4 over the
-// current 4^3 brick.  One code path for both, so a wave whose lanes mix
-// cell steps and brick skips pays for one of them, not both.  CROSSED: the
-// new cell lies in another brick.  EXITED: the walk left the grid (T_EXIT is
-// then +inf, as Iterator.next returns at the exit cell).
-#define ADV_AXIS(S, G, A, BR)                                                                 \
-    const bool n##A##_ = ((S).neg >> A) & 1u;                                                 \
-    const uint32_t lo##A##_ = (BR) ? ((S).c##A & ~3u) : (S).c##A;                             \
-    const uint32_t hi##A##_ = (BR) ? zmin(((S).c##A & ~3u) + 3u, (G).rm##A) : (S).c##A;       \
-    const uint32_t m##A##_ = n##A##_ ? (S).c##A - lo##A##_ + 1u : hi##A##_ - (S).c##A + 1u;   \
-    const bool out##A##_ = n##A##_ ? lo##A##_ == 0u : hi##A##_ == (G).rm##A;                  \
-    const float T##A##1_ = (S).tn##A;                                                         \
-    const float T##A##2_ = T##A##1_ + (S).td##A;                                              \
-    const float T##A##3_ = T##A##2_ + (S).td##A;                                              \
-    const float T##A##4_ = T##A##3_ + (S).td##A;                                              \
-    const uint32_t mm##A##_ = m##A##_ - 1u;                                                   \
-    const float E##A##_ = (mm##A##_ & 2u) ? ((mm##A##_ & 1u) ? T##A##4_ : T##A##3_)           \
-                                          : ((mm##A##_ & 1u) ? T##A##2_ : T##A##1_);
-#define ADV_COUNT(S, A, TIE)                                                                  \
-    const bool ti##A##_ = (TIE);                                                              \
-    uint32_t k##A##_ = (uint32_t)((1u < m##A##_) & ((T##A##1_ < ex_) | ((T##A##1_ == ex_) & ti##A##_))) + \
-                       (uint32_t)((2u < m##A##_) & ((T##A##2_ < ex_) | ((T##A##2_ == ex_) & ti##A##_))) + \
-                       (uint32_t)((3u < m##A##_) & ((T##A##3_ < ex_) | ((T##A##3_ == ex_) & ti##A##_)));  \
-    k##A##_ = x##A##_ ? m##A##_ : k##A##_;                                                    \
-    const float T##A##5_ = T##A##4_ + (S).td##A;                                              \
-    const float L##A##a_ = (k##A##_ & 1u) ? T##A##2_ : T##A##1_;                              \
-    const float L##A##b_ = (k##A##_ & 1u) ? T##A##4_ : T##A##3_;                              \
-    const float L##A##c_ = (k##A##_ & 2u) ? L##A##b_ : L##A##a_;                              \
-    (S).tn##A = (k##A##_ & 4u) ? T##A##5_ : L##A##c_;                                         \
-    const uint32_t o##A##_ = (S).c##A;                                                        \
-    (S).c##A = n##A##_ ? (S).c##A - k##A##_ : (S).c##A + k##A##_;
-#define DDA_ADVANCE(S, G, BR, CROSSED, EXITED, T_EXIT)                                        \
-    do {                                                                                      \
-        ADV_AXIS(S, G, 0, BR)                                                                 \
-        ADV_AXIS(S, G, 1, BR)                                                                 \
-        ADV_AXIS(S, G, 2, BR)                                                                 \
-        const bool x0_ = (E0_ < E1_) & (E0_ < E2_);                                           \
-        const bool x1_ = !(E0_ < E1_) & (E1_ < E2_);                                          \
-        const bool x2_ = !x0_ & !x1_;                                                         \
-        const float ex_ = x0_ ? E0_ : (x1_ ? E1_ : E2_);                                      \
-        ADV_COUNT(S, 0, false)                                                                \
-        ADV_COUNT(S, 1, x0_)                                                                  \
-        ADV_COUNT(S, 2, !x2_)                                                                 \
-        (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                       \
-        (T_EXIT) = (EXITED) ? kInf : ex_;                                                     \
-        (CROSSED) = (((o0_ ^ (S).c0) | (o1_ ^ (S).c1) | (o2_ ^ (S).c2)) >> 2) != 0u;          \
         (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
     } while (0)
 

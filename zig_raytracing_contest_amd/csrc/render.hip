@@ -187,162 +187,6 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
     }
 }
 
-// test_cell for the park kernel's test rounds: branch-free tests (the lanes
-// of a round test different triangles, so tri_ray's early returns would only
-// add divergent branches), nearest/(u, v)/ref updated by selects.
-template <int TB>
-__device__ __forceinline__ void test_cell_flat(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
-                                               float& nearest, float& hu, float& hv, uint32_t& hidx) {
-    for (uint32_t i = b; i < e; i += TB) {
-        float4 A[TB], Bq[TB], Cq[TB];
-#pragma unroll
-        for (int k = 0; k < TB; ++k) {
-            const uint32_t j = min(i + (uint32_t)k, e - 1u);
-            A[k] = p.tri_pos[3 * j + 0];
-            Bq[k] = p.tri_pos[3 * j + 1];
-            Cq[k] = p.tri_pos[3 * j + 2];
-        }
-#pragma unroll
-        for (int k = 0; k < TB; ++k) {
-            float t, u, v;
-            const bool hit = tri_ray_flat(mk(A[k].x, A[k].y, A[k].z), mk(Bq[k].x, Bq[k].y, Bq[k].z),
-                                          mk(Cq[k].x, Cq[k].y, Cq[k].z), o, d, &t, &u, &v);
-            // stage3.zig:172 `nearest > t and t > 0`, in reference order
-            const bool acc = (i + (uint32_t)k < e) & hit & (nearest > t) & (t > 0.0f);
-            nearest = acc ? t : nearest;
-            hu = acc ? u : hu;
-            hv = acc ? v : hv;
-            hidx = acc ? i + (uint32_t)k : hidx;
-        }
-    }
-}
-
-// Lane gathers (ds_bpermute: lane reads `x` of lane `src`) and the forward
-// permute (ds_permute: lane pushes `x` to lane `dst`).  Called with the whole
-// wave active.
-__device__ __forceinline__ uint32_t lane_get(uint32_t x, uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)x);
-}
-__device__ __forceinline__ float lane_getf(float x, uint32_t src) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(x)));
-}
-__device__ __forceinline__ uint32_t lane_put(uint32_t x, uint32_t dst) {
-    return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)x);
-}
-
-// DPP lane moves (row_shr:k within rows of 16, row_bcast:15 / :31 across
-// rows): the wave scans below cost VALU cycles, not LDS round trips.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
-}
-// Inclusive wave scans: sum, max.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
-    const uint32_t rl = lane & 15u;
-    x += rl >= 1u ? dpp<0x111>(x) : 0u;
-    x += rl >= 2u ? dpp<0x112>(x) : 0u;
-    x += rl >= 4u ? dpp<0x114>(x) : 0u;
-    x += rl >= 8u ? dpp<0x118>(x) : 0u;
-    x += (lane & 31u) >= 16u ? dpp<0x142>(x) : 0u;
-    x += lane >= 32u ? dpp<0x143>(x) : 0u;
-    return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x, uint32_t lane) {
-    const uint32_t rl = lane & 15u;
-    x = rl >= 1u ? max(x, dpp<0x111>(x)) : x;
-    x = rl >= 2u ? max(x, dpp<0x112>(x)) : x;
-    x = rl >= 4u ? max(x, dpp<0x114>(x)) : x;
-    x = rl >= 8u ? max(x, dpp<0x118>(x)) : x;
-    x = (lane & 31u) >= 16u ? max(x, dpp<0x142>(x)) : x;
-    x = lane >= 32u ? max(x, dpp<0x143>(x)) : x;
-    return x;
-}
-// One step of the segmented (per owner) lexicographic min-scan of (hi, lo).
-template <int CTRL>
-__device__ __forceinline__ void seg_min_step(bool on, uint32_t ow, uint32_t& hi, uint32_t& lo) {
-    const uint32_t h = dpp<CTRL>(hi), l = dpp<CTRL>(lo), o = dpp<CTRL>(ow);
-    const bool take = on & (o == ow) & ((h < hi) | ((h == hi) & (l < lo)));
-    hi = take ? h : hi;
-    lo = take ? l : lo;
-}
-
-// One test round of the park kernel, the wave's (cell, triangle) pairs
-// spread over all 64 lanes (the whole wave must be active).
-//
-// Lane i owns n_i = pe - pb triangles (0 if it is not parked).  The pairs are
-// laid out in lane order (owner i covers pair slots [off_i, off_i + n_i)) and
-// tested 64 at a time, lane q taking slot r + q: one triangle load per lane
-// per sub-round, all in flight together, instead of each parked lane walking
-// its own cell while most lanes idle.  Per owner the result is the
-// lexicographic min of (t, ref) over its pairs with 0 < t < nearest - exactly
-// what the reference's in-order `nearest > t and t > 0` loop keeps
-// (stage3.zig:164-178: the smallest t, the first ref among equal t).  t > 0
-// orders like its bit pattern, so the key is (t bits, ref), reduced by a
-// segmented min-scan across lanes; (u, v) come from the winning lane.
-// `mark`: this wave's 64-byte LDS scratch (owner starts of a sub-round).
-__device__ __forceinline__ void test_round_wave(const TraceParams& p, uint8_t* mark, bool parked, uint32_t pb,
-                                                uint32_t pe, v3 o, v3 d, float& nearest, float& hu, float& hv,
-                                                uint32_t& hidx) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nl = parked ? pe - pb : 0u;
-    const uint32_t incl = wave_incl_sum(nl, lane);
-    const uint32_t off = incl - nl;
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    unsigned long long best = ~0ull;
-    float bu = 0.0f, bv = 0.0f;
-    uint32_t carry = 0;
-    for (uint32_t r = 0; r < total; r += 64u) {
-        // owner of slot r + lane: the last owner starting at or before it
-        mark[lane] = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (nl != 0u && off >= r && off < r + 64u) mark[off - r] = (uint8_t)(lane + 1u);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t m = wave_incl_max(mark[lane], lane);
-        const uint32_t ow = m != 0u ? m - 1u : carry;
-        carry = __builtin_amdgcn_readlane(ow, 63);
-        const uint32_t g = r + lane;
-        const uint32_t j = lane_get(pb, ow) + (g - lane_get(off, ow));
-        const v3 ro = mk(lane_getf(o.x, ow), lane_getf(o.y, ow), lane_getf(o.z, ow));
-        const v3 rd = mk(lane_getf(d.x, ow), lane_getf(d.y, ow), lane_getf(d.z, ow));
-        const float nb = lane_getf(nearest, ow);
-        const bool valid = g < total;
-        const uint32_t jj = valid ? j : 0u;
-        const float4 A = p.tri_pos[3ull * jj], Bq = p.tri_pos[3ull * jj + 1], Cq = p.tri_pos[3ull * jj + 2];
-        float t, u, v;
-        const bool hit = tri_ray_flat(mk(A.x, A.y, A.z), mk(Bq.x, Bq.y, Bq.z), mk(Cq.x, Cq.y, Cq.z), ro, rd,
-                                      &t, &u, &v);
-        const bool acc = valid & hit & (nb > t) & (t > 0.0f);     // stage3.zig:172
-        uint32_t khi = acc ? __float_as_uint(t) : 0xFFFFFFFFu;
-        uint32_t klo = acc ? j : 0xFFFFFFFFu;
-        // segmented inclusive min-scan: the last lane of each owner's run
-        // in this sub-round ends up with the run's min
-        const uint32_t rl = lane & 15u;
-        seg_min_step<0x111>(rl >= 1u, ow, khi, klo);
-        seg_min_step<0x112>(rl >= 2u, ow, khi, klo);
-        seg_min_step<0x114>(rl >= 4u, ow, khi, klo);
-        seg_min_step<0x118>(rl >= 8u, ow, khi, klo);
-        seg_min_step<0x142>((lane & 31u) >= 16u, ow, khi, klo);
-        seg_min_step<0x143>(lane >= 32u, ow, khi, klo);
-        // owners: their run's last lane in this sub-round
-        const bool mine = (nl != 0u) & (off < r + 64u) & (off + nl > r);
-        const uint32_t last = (min(off + nl, r + 64u) - 1u - r) & 63u;
-        const uint32_t rh = lane_get(khi, last), rlo = lane_get(klo, last);
-        const uint32_t wl = (rlo - pb + off - r) & 63u;             // the winning lane
-        const float ru = lane_getf(u, wl), rv = lane_getf(v, wl);
-        const unsigned long long rk = ((unsigned long long)rh << 32) | rlo;
-        const bool better = mine & (rk < best);
-        best = better ? rk : best;
-        bu = better ? ru : bu;
-        bv = better ? rv : bv;
-    }
-    if (parked && best != ~0ull) {
-        nearest = __uint_as_float((uint32_t)(best >> 32));
-        hidx = (uint32_t)best;
-        hu = bu;
-        hv = bv;
-    }
-}
-
 // Diagnostic build only (ZRT_PROFILE=1): s_memtime stamps apportion each
 // wave's cycles to code regions.  Never in the timed kernel.
 __device__ __forceinline__ uint64_t stamp() {
@@ -693,12 +537,6 @@ struct WfParams {
     uint32_t refill;          // split mode: idle lanes before a wave fetches rays
     uint32_t* hist;           // ray sort: per-key counts of the appended paths (null: no sort)
     uint32_t sort_bits;       // ray sort: origin-region bits per axis
-    // park mode: exact per-cell occupancy blob (see OccX) and its layout
-    const uint32_t* occx;
-    uint32_t occx_words, occx_nbw, occx_moff, occx_nb0, occx_nb01;
-    uint32_t test_min;        // park mode: parked lanes before a wave runs a test round
-    uint32_t skip_min;        // park mode: lanes in empty bricks before a wave skips bricks
-    uint32_t coop;            // park mode: wave-cooperative test rounds (test_round_wave)
 };
 
 // Ray-sort key of a continuing path: the origin's region in a 2^R per axis
@@ -1034,266 +872,6 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfPar
     }
 }
 
-// ---------------------------------------------------------------------------
-// Park mode (default): Scene.traceRay as walk / park / test rounds.
-//
-// Counted on the contest stand-in (cfg3): a segment visits 85 cells, 4.3 of
-// them non-empty.  A wave that walks its 64 rays in lockstep and loads a cell
-// whenever its lane needs one pays a global-load round trip in nearly every
-// step (some lane of 64 is almost always at a non-empty cell), so the walk
-// runs at memory latency although it is arithmetic.  Here:
-//  * the exact per-cell occupancy sits in LDS (OccX), so an empty cell costs
-//    DDA arithmetic and, when a 4^3 brick is entered, two LDS reads - never a
-//    global load;
-//  * a lane that reaches a non-empty cell P issues the load of P's range and
-//    keeps walking to the NEXT non-empty cell N (the load's latency hides
-//    behind that walk), folding the exit t of every cell it passes into B;
-//    then it parks;
-//  * once `test_min` lanes are parked (or nobody walks) the wave runs one
-//    test round: every parked lane tests P's triangles in reference order,
-//    then ends the segment if traceRay would have broken in [P, N), else
-//    makes N its pending cell and walks on.  Finished lanes store the hit
-//    record and take fresh rays (refill), shading runs in wf_shade_kernel.
-//
-// Equivalence with traceRay's loop (stage3.zig:160-183), cell by cell: the
-// loop tests cell k, then breaks if nearest <= t_exit(k).  Between P and N
-// the cells are empty, so nearest is constant there and "breaks in [P, N)"
-// is nearest <= max t_exit over [P, N) (fmaxf drops NaN exactly as `<=`
-// against NaN is false; the grid exit's +inf always breaks).  The walk may
-// stop early (`fin`) once the PRE-test nearest already satisfies
-// nearest <= t_exit: testing P can only lower it, so the break in [P, N) is
-// certain and the result is nearest after P.  Before the first non-empty
-// cell nearest is +inf and only the grid exit ends the walk.  Same cells,
-// same tests in the same order, same hit.
-//
-// OccX (shift 2 bricks): bit per brick, u16 number of occupied bricks before
-// each 32-brick word, one 64-bit cell mask per occupied brick (+ one zero).
-struct OccX {
-    const uint32_t* bits;
-    const uint16_t* prefix;
-    const unsigned long long* masks;
-};
-__device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
-    const uint32_t wd = L.bits[b >> 5];
-    const uint32_t r = (uint32_t)L.prefix[b >> 5] + (uint32_t)__popc(wd & ((1u << (b & 31u)) - 1u));
-    const unsigned long long m = L.masks[r];            // r <= occupied count: the zero pad at worst
-    return ((wd >> (b & 31u)) & 1u) ? m : 0ull;
-}
-__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const Dda& s) {
-    return (s.c2 >> 2) * w.occx_nb01 + (s.c1 >> 2) * w.occx_nb0 + (s.c0 >> 2);
-}
-__device__ __forceinline__ uint32_t occx_bit(const Dda& s) {
-    return ((s.c2 & 3u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
-}
-
-// Range of the pending cell: loaded by LDS-DMA (global_load_lds) into this
-// wave's two 64-dword slots (begin | end per lane), so no VGPR waits on it
-// while the lane walks on; the test round waits (vmcnt) and reads it back.
-__device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t lin, uint32_t* slot) {
-    const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells) + 2ull * lin;
-    __builtin_amdgcn_global_load_lds(c, slot, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds(c + 1, slot + 64, 4, 0, 0);
-}
-
-constexpr int kParkMaxWaves = 16;   // waves per workgroup (1024 threads)
-
-// CNT (diagnostic build, ZRT_PARK_STATS): wave-level schedule counters.
-//
-// Lane states: Idle (no path), Walk, Park (see above), Done (the segment's
-// hit is known and waits for shading).  Shading - traceRayRecursive's body
-// after traceRay (stage3.zig:195-219) - runs in rounds too: once `refill`
-// lanes are Done or Idle, the Done lanes shade together (texture fetches,
-// ziggurat draws, the bounce-stack store, the append of continuing paths to
-// the next queue) and then every Idle lane takes a fresh path.
-template <int TB, bool PRIMARY, bool CNT = false, int MINW = 6>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MINW, 8)))
-void wf_park_kernel(const WfParams w) {
-    const TraceParams& p = w.t;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    __shared__ uint32_t s_range[kParkMaxWaves * 128];
-    __shared__ uint8_t s_mark[kParkMaxWaves * 64];
-    __shared__ double s_zig[514];
-    for (uint32_t i = threadIdx.x; i < w.occx_words; i += blockDim.x) s_occ[i] = w.occx[i];
-    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
-    __syncthreads();
-    OccX L;
-    L.bits = s_occ;
-    L.prefix = reinterpret_cast<const uint16_t*>(s_occ + w.occx_nbw);
-    L.masks = reinterpret_cast<const unsigned long long*>(s_occ + w.occx_moff);
-    uint32_t* slot = s_range + 128u * (threadIdx.x >> 6);     // wave-uniform LDS-DMA base
-    const double* zx = s_zig;
-    const double* zf = s_zig + 257;
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t n = PRIMARY ? p.total : *w.n_in;
-    const uint32_t refill = w.refill, test_min = w.test_min;
-    const GridK gk = grid_consts(p);
-    constexpr uint32_t kIdle = 0, kWalk = 1, kPark = 2, kDone = 3;
-    uint32_t st = kIdle;
-    bool more = n != 0, hasP = false, fin = false;
-    float B = -kInf, nearest = kInf, hu = 0.0f, hv = 0.0f;
-    uint32_t hidx = 0;
-    unsigned long long bm = 0ull;
-    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    // the path (traceRayRecursive's recursion state)
-    uint32_t item = 0, depth = 0, pslot = 0, mask = 0;
-    Rng rng;
-    rng.s = 0;
-    Dda s;
-    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
-    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
-    Mailbox mbx;
-    mbx.reset();
-    uint32_t n_seg = 0;
-    // walk iters, walking lanes, test rounds, parked lanes, tri-batch trips,
-    // refills, outer iterations, lanes alive at walk start
-    // + s_memtime cycles: range wait, test round, shade+refill, walk
-    unsigned long long cnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (;;) {
-        if (CNT) ++cnt[6];
-        uint64_t tA = CNT ? stamp() : 0;
-        // ---- test round: every parked lane tests its pending cell
-        if (__ballot(st == kPark) != 0ull) {
-            __builtin_amdgcn_s_waitcnt(0x3f70);                    // vmcnt(0): ranges landed
-            if (CNT) { const uint64_t t = stamp(); cnt[8] += t - tA; tA = t; }
-            if (CNT) { ++cnt[2]; cnt[3] += (uint64_t)__popcll(__ballot(st == kPark)); }
-            if (CNT && st == kPark) {
-                const uint32_t nb = (slot[64 + lane] - slot[lane] + TB - 1) / TB;
-                uint32_t mx = nb;
-                for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-                if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) cnt[4] += mx;
-            }
-            const bool parked = st == kPark;
-            const uint32_t pb = slot[lane], pe = slot[64 + lane];
-            if (w.coop) test_round_wave(p, s_mark + 64u * (threadIdx.x >> 6), parked, pb, pe, o, d, nearest, hu, hv, hidx);
-            else if (parked) test_cell_flat<TB>(p, pb, pe, o, d, nearest, hu, hv, hidx);
-            if (parked) {
-                if (fin || nearest <= B) {
-                    st = kDone;
-                } else {                                           // N becomes pending
-                    park_load_range(p, s.lin, slot);
-                    B = -kInf;
-                    st = kWalk;
-                }
-            }
-        }
-        if (CNT) { const uint64_t t = stamp(); cnt[9] += t - tA; tA = t; }
-        // ---- shade + refill round, once enough lanes are Done or Idle
-        const uint64_t ready = __ballot(st == kIdle || st == kDone);
-        const uint32_t nready = (uint32_t)__popcll(ready);
-        if (nready >= refill || nready == 64u || (ready != 0ull && __ballot(st == kWalk || st == kPark) == 0ull)) {
-            if (__ballot(st == kDone) != 0ull) {
-                bool cont = false;
-                if (st == kDone) {                                 // stage3.zig:195-219
-                    ++n_seg;
-                    v3 Lr = mk(0, 0, 0);
-                    cont = shade_segment(w, zx, zf, item, nearest, hu, hv, hidx, o, d, depth, pslot, rng, mask,
-                                         Lr);
-                    if (!cont) w.term[item] = make_float4(Lr.x, Lr.y, Lr.z, __uint_as_float(mask));
-                    st = kIdle;
-                }
-                wf_append(w, cont, below, o, d, item, depth, pslot, rng, mask);
-            }
-            const uint64_t idle = __ballot(st == kIdle);
-            const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (more && nidle != 0u) {
-                uint32_t base = 0;
-                if (CNT) ++cnt[5];
-                if (lane == 0) base = atomicAdd(w.fetch, nidle);
-                base = __builtin_amdgcn_readfirstlane(base);
-                more = base < n && n - base > nidle;
-                if (st == kIdle) {
-                    const uint32_t r = base + (uint32_t)__popcll(idle & below);
-                    if (base < n && r < n) {
-                        if (PRIMARY) {
-                            item = r;
-                            camera_ray(p, r, rng, o, d);
-                            depth = p.max_bounce;
-                            pslot = 0;
-                            mask = 0;
-                        } else {
-                            const float4 qa = w.q_in[3ull * r], qb = w.q_in[3ull * r + 1], qc = w.q_in[3ull * r + 2];
-                            o = mk(qa.x, qa.y, qa.z);
-                            item = __float_as_uint(qa.w);
-                            d = mk(qb.x, qb.y, qb.z);
-                            depth = __float_as_uint(qb.w) & 0xFFFFu;
-                            pslot = __float_as_uint(qb.w) >> 16;
-                            rng.s = ((uint64_t)__float_as_uint(qc.y) << 32) | __float_as_uint(qc.x);
-                            mask = __float_as_uint(qc.z);
-                        }
-                        nearest = kInf;
-                        hu = hv = 0.0f;
-                        hidx = 0;
-                        hasP = fin = false;
-                        B = -kInf;
-                        if (depth == 0u) {                         // max_bounce 0: black, nothing traced
-                            w.term[item] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(mask));
-                        } else if (dda_setup(p, o, d, s)) {        // stage3.zig:153-156
-                            st = kWalk;
-                            bm = occx_mask(L, occx_brick(w, s));
-                            if ((bm >> occx_bit(s)) & 1ull) {
-                                hasP = true;
-                                park_load_range(p, s.lin, slot);
-                            }
-                        } else {
-                            st = kDone;                            // misses the grid: nearest = +inf
-                        }
-                    }
-                }
-            }
-        }
-        if (CNT) { const uint64_t t = stamp(); cnt[10] += t - tA; tA = t; }
-        if (__ballot(st != kIdle) == 0ull) {
-            if (!more) break;
-            continue;
-        }
-        // ---- walk until test_min lanes are parked or nobody walks
-        for (;;) {
-            const uint64_t wk = __ballot(st == kWalk);
-            if (wk == 0ull || (uint32_t)__popcll(__ballot(st == kPark)) >= test_min) break;
-            // brick skips (DDA_ADVANCE, ~4x a cell step) only when enough
-            // walking lanes are in empty bricks; otherwise everyone steps one cell
-            const bool use_adv =
-                (uint32_t)__popcll(__ballot(st == kWalk && bm == 0ull && s.neg < 8u)) >= w.skip_min;
-            if (CNT) { ++cnt[0]; cnt[1] += (uint64_t)__popcll(wk); cnt[7] += (uint64_t)__popcll(__ballot(st != kIdle)); }
-            if (st == kWalk) {
-                // an empty brick is crossed in one advance (dda.h DDA_ADVANCE:
-                // the state and the largest exit t Iterator.next would reach)
-                bool crossed, exited;
-                float te;
-                const bool br = bm == 0ull && s.neg < 8u;
-                if (use_adv) {
-                    DDA_ADVANCE(s, gk, br, crossed, exited, te);
-                } else {
-                    DDA_STEP(s, gk, 2u, crossed, te);
-                }
-                B = fmaxf(B, te);
-                if (te == kInf || nearest <= te) {                 // stage3.zig:179-182
-                    fin = true;
-                    st = hasP ? kPark : kDone;                     // no pending cell: nearest is +inf
-                } else {
-                    if (crossed) bm = occx_mask(L, occx_brick(w, s));
-                    if ((bm >> occx_bit(s)) & 1ull) {
-                        if (hasP) {
-                            st = kPark;
-                        } else {
-                            hasP = true;
-                            park_load_range(p, s.lin, slot);
-                            B = -kInf;
-                        }
-                    }
-                }
-            }
-        }
-        if (CNT) cnt[11] += stamp() - tA;
-    }
-    const unsigned long long s0 = wave_sum(n_seg);
-    if (lane == 0) atomicAdd(&p.stats[0], s0);
-    if (CNT && lane == 0)
-        for (int i = 0; i < 12; ++i) atomicAdd(&p.stats[16 + i], cnt[i]);
-}
-
 template <bool PRIMARY>
 __global__ __launch_bounds__(kBlock) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
@@ -1465,7 +1043,9 @@ using TraceFn = void (*)(const TraceParams);
 // few spills land outside the DDA loop and 6 waves hide more memory latency
 // than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
 constexpr int kMinWaves = 6;
-constexpr int kWfMinWaves = 6;
+// wf_kernel: 7 waves/SIMD (72 VGPRs): cfg3 64 spp 1826 vs 1786 and 1783 vs
+// 1775 Mrays/s against 6 in two r01 sweeps; 8 (64 VGPRs) spills: 1503.
+constexpr int kWfMinWaves = 7;
 constexpr int kSplitMinWaves = 6;
 
 template <int MAXB>
@@ -1532,9 +1112,6 @@ struct zrt_context {
     double* d_zig = nullptr;
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
-    uint32_t* d_occx = nullptr;     // park mode: exact per-cell occupancy blob (OccX)
-    uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
-    bool occx_ok = false;
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;
@@ -1597,7 +1174,7 @@ extern "C" int zrt_device_count(int* count) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_pix,
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
                     c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_hit, c->d_hist, c->d_cursor, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1718,53 +1295,6 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
         HIP_TRY(hipMalloc((void**)&c->d_occ, bits.size() * 4));
         HIP_TRY(hipMemcpy(c->d_occ, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
     }
-    // park mode: exact per-cell occupancy over 4^3-cell bricks (OccX layout:
-    // bits | u16 prefix per 32-brick word | u64 cell mask per occupied brick + 0)
-    {
-        const uint32_t* r = s->grid.resolution;
-        for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
-        const uint64_t nb = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
-        const uint64_t nbw = (nb + 31) / 32;
-        std::vector<unsigned long long> mask(nb, 0ull);
-        for (uint32_t z = 0; z < r[2]; ++z)
-            for (uint32_t y = 0; y < r[1]; ++y)
-                for (uint32_t x = 0; x < r[0]; ++x) {
-                    const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
-                    if (s->cells[2 * ci] < s->cells[2 * ci + 1]) {
-                        const uint64_t b = ((uint64_t)(z >> 2) * c->occx_nb[1] + (y >> 2)) * c->occx_nb[0] + (x >> 2);
-                        mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
-                    }
-                }
-        std::vector<uint32_t> bits(nbw, 0u);
-        std::vector<uint16_t> prefix(nbw, 0);
-        std::vector<unsigned long long> masks;
-        uint64_t run = 0;
-        for (uint64_t wd = 0; wd < nbw; ++wd) {
-            prefix[wd] = (uint16_t)std::min<uint64_t>(run, 0xFFFF);
-            for (uint64_t b = wd * 32; b < std::min<uint64_t>(nb, wd * 32 + 32); ++b)
-                if (mask[b]) { bits[wd] |= 1u << (b & 31); masks.push_back(mask[b]); ++run; }
-        }
-        masks.push_back(0ull);
-        const uint64_t pw = (nbw + 1) / 2;                   // prefix words
-        const uint64_t moff = (nbw + pw + 1) & ~1ull;        // masks 8-byte aligned
-        const uint64_t words = moff + 2 * masks.size();
-        // LDS budget: two park workgroups per CU (80 KiB each) hold this
-        // blob + their static LDS (LDS-DMA range slots, ziggurat tables)
-        size_t budget = 80 * 1024 - 16 * 128 * 4 - 16 * 64 - 514 * 8;
-        if (const char* e = getenv("ZRT_OCCX_BYTES")) budget = (size_t)atoll(e);
-        c->occx_ok = run < 0xFFFF && nb < (1ull << 32) && words * 4 <= budget;
-        if (c->occx_ok) {
-            std::vector<uint32_t> blob(words, 0u);
-            memcpy(blob.data(), bits.data(), nbw * 4);
-            memcpy(blob.data() + nbw, prefix.data(), nbw * 2);
-            memcpy(blob.data() + moff, masks.data(), masks.size() * 8);
-            c->occx_words = (uint32_t)words;
-            c->occx_nbw = (uint32_t)nbw;
-            c->occx_moff = (uint32_t)moff;
-            HIP_TRY(hipMalloc((void**)&c->d_occx, words * 4));
-            HIP_TRY(hipMemcpy(c->d_occx, blob.data(), words * 4, hipMemcpyHostToDevice));
-        }
-    }
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
     return ZRT_OK;
@@ -1842,9 +1372,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const bool wf = !want_stats && !want_prof && !(mode_env && strcmp(mode_env, "mega") == 0);
     // "wf" (default): one fused trace+shade kernel per bounce; "split":
     // wf_trace_kernel (lane refill) + wf_shade_kernel per bounce
-    // "park": wf_park_kernel (walk / park / test / shade rounds in one kernel);
-    // needs the exact occupancy blob (fits the LDS budget)
-    const bool park = wf && c->occx_ok && mode_env && strcmp(mode_env, "park") == 0;
     const bool split = wf && mode_env && strcmp(mode_env, "split") == 0;
     // per-item bytes of a pass: megakernel = the float4 sample radiance;
     // wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per bounce
@@ -1885,18 +1412,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
 
     // occupancy-sized persistent grids
-    int tblock = trace_block();
-    // park: waves per SIMD the kernel is compiled for (VGPR budget 80 / 96)
-    int park_w = 6;
-    if (const char* e = getenv("ZRT_PARK_W")) park_w = atoi(e) == 5 ? 5 : 6;
-    if (park) {                 // two workgroups per CU of 2*park_w waves: park_w waves per SIMD
-        tblock = 128 * park_w;
-        if (const char* e = getenv("ZRT_PARK_BLOCK")) tblock = std::max(64, std::min(1024, atoi(e) / 64 * 64));
-    }
+    const int tblock = trace_block();
     const char* wave_env = getenv("ZRT_WAVE");
     const bool wave_mode = wf && !split && wave_env && atoi(wave_env) == 1;
-    const size_t lds_bytes = park ? 4ull * c->occx_words
-                           : wave_mode ? 16ull * ((c->occ_words + 3u) / 4u) + (size_t)(tblock / 64) * sizeof(WaveLds)
+    const size_t lds_bytes = wave_mode ? 16ull * ((c->occ_words + 3u) / 4u) + (size_t)(tblock / 64) * sizeof(WaveLds)
                                        : 4ull * c->occ_words;
     auto grid_for = [&](const void* f, uint32_t* blocks) -> int {
         int bpc = 0;
@@ -1935,15 +1454,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             if (mw == 5) { wf_first = (WfFn)wf_wave_kernel<5, true>; wf_next = (WfFn)wf_wave_kernel<5, false>; }
             else if (mw == 8) { wf_first = (WfFn)wf_wave_kernel<8, true>; wf_next = (WfFn)wf_wave_kernel<8, false>; }
             else { wf_first = (WfFn)wf_wave_kernel<6, true>; wf_next = (WfFn)wf_wave_kernel<6, false>; }
-        } else if (park && getenv("ZRT_PARK_STATS")) {
-            wf_first = (WfFn)wf_park_kernel<kTriBatch, true, true>;
-            wf_next = (WfFn)wf_park_kernel<kTriBatch, false, true>;
-        } else if (park && park_w == 5) {
-            wf_first = (WfFn)wf_park_kernel<kTriBatch, true, false, 5>;
-            wf_next = (WfFn)wf_park_kernel<kTriBatch, false, false, 5>;
-        } else if (park) {
-            wf_first = (WfFn)wf_park_kernel<kTriBatch, true>;
-            wf_next = (WfFn)wf_park_kernel<kTriBatch, false>;
         } else if (split) {
             ZRT_WF_SWITCH(wf_trace_kernel)
         } else if (mbe && atoi(mbe) == 1) {
@@ -1973,12 +1483,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_cursor, &c->cursor_cap, nbins)) != ZRT_OK) return rc;
     }
     if (const char* e = getenv("ZRT_REFILL")) refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    uint32_t coop = 1;
-    if (const char* e = getenv("ZRT_COOP")) coop = atoi(e) ? 1u : 0u;
-    uint32_t skip_min = 24;
-    if (const char* e = getenv("ZRT_SKIP_MIN")) skip_min = (uint32_t)std::max(1, std::min(65, atoi(e)));
-    uint32_t test_min = 16;
-    if (const char* e = getenv("ZRT_TEST_MIN")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     const uint32_t shade_blocks = (uint32_t)c->num_cus * 8u;
 
     TraceParams tp;
@@ -2037,15 +1541,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.T = (uint32_t)T;
             W.refill = refill;
             W.sort_bits = sort_bits;
-            W.occx = c->d_occx;
-            W.occx_words = c->occx_words;
-            W.occx_nbw = c->occx_nbw;
-            W.occx_moff = c->occx_moff;
-            W.occx_nb0 = c->occx_nb[0];
-            W.occx_nb01 = c->occx_nb[0] * c->occx_nb[1];
-            W.test_min = test_min;
-            W.skip_min = skip_min;
-            W.coop = coop;
             const uint32_t nb = std::max<uint32_t>(mb, 1);
             if (sorting) HIP_TRY(hipMemsetAsync(c->d_hist, 0, 4ull * nbins, c->stream));
             for (uint32_t k = 0; k < nb; ++k) {
@@ -2118,11 +1613,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu, "
                 "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu, \"trips_with_tests\": %llu, \"shared_rounds\": %llu}}\n",
                 hs[1], hs[4], hs[5], hs[2], hs[6], hs[7], hs[14], hs[15]);
-    if (park && getenv("ZRT_PARK_STATS"))
-        fprintf(stderr, "{\"zrt_park\": {\"walk_iters\": %llu, \"walk_lanes\": %llu, \"test_rounds\": %llu, "
-                "\"test_lanes\": %llu, \"tri_trips\": %llu, \"refills\": %llu, \"outer\": %llu, \"alive_lanes\": %llu, "
-                "\"cyc_wait\": %llu, \"cyc_test\": %llu, \"cyc_refill\": %llu, \"cyc_walk\": %llu}}\n",
-                hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27]);
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
