@@ -11,7 +11,7 @@ OBJ       := build/obj
 HIPFLAGS  := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
              -Wall -Wno-unused-function -Iinclude
 CXXFLAGS  := -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Iinclude -pthread
-HDRS      := include/zrt.h $(SRC)/zrt_math.h $(SRC)/zrt_internal.h $(SRC)/dda.h
+HDRS      := include/zrt.h $(SRC)/zrt_math.h $(SRC)/zrt_internal.h $(SRC)/dda.h $(SRC)/geometry.h
 HOST_SRCS := $(filter-out $(SRC)/cli.cpp,$(wildcard $(SRC)/*.cpp))
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(HOST_SRCS))
 LIB       := $(PKG)/libzrt.so
@@ -23,11 +23,13 @@ $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) $(wildcard $(SRC)/*.h)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(OBJ)/render.o: $(SRC)/render.hip $(HDRS)
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJ)/render.o $(HOST_OBJS)
+HIP_OBJS  := $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
+
+$(LIB): $(HIP_OBJS) $(HOST_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lz -pthread
 
 $(CLI): $(SRC)/cli.cpp $(LIB) include/zrt.h

@@ -137,6 +137,14 @@ typedef struct zrt_geometry zrt_geometry;
 int zrt_geometry_build(const float* positions, const float* normals, const float* texcoords,
                        const uint32_t* material, uint32_t num_triangles,
                        const uint32_t resolution[3], uint32_t num_threads, zrt_geometry** out);
+/* The same build on a GPU: SAT binning, cell order and
+ * bake as HIP kernels on device `device` (-1 = current).  Output identical
+ * to zrt_geometry_build, bit for bit; the result lives in host memory like
+ * the host build's.  Replaces Geometry.build + bakeInto (stage2.zig:131-164,
+ * called at main.zig:117-118). */
+int zrt_geometry_build_device(const float* positions, const float* normals, const float* texcoords,
+                              const uint32_t* material, uint32_t num_triangles,
+                              const uint32_t resolution[3], int device, zrt_geometry** out);
 /* Fills grid/cells/triangle arrays of *scene (views into the geometry,
  * valid until zrt_geometry_free); leaves the material fields untouched. */
 int zrt_geometry_scene(const zrt_geometry* g, zrt_scene* scene);

@@ -1,0 +1,41 @@
+"""GPU grid build (csrc/grid_build.hip) against the host
+build (geometry.cpp, itself pinned to the oracle by test_build_parity.py):
+grid, cells, ref order and every baked array, bit for bit."""
+import time
+
+import numpy as np
+import pytest
+
+from zig_raytracing_contest_amd import native, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,res", [("sphere", (128, 128, 128)), ("sphere", (5, 7, 3)),
+                                      ("cornell", (128, 128, 128)), ("cornell555", (128, 128, 128)),
+                                      ("contest", (128, 128, 128)), ("contest", (1, 1, 1)),
+                                      ("sponza", (128, 128, 128)), ("sponza", (200, 64, 97))])
+def test_device_build_bitexact(name, res):
+    soup = scenes.get_scene(name)
+    t0 = time.perf_counter()
+    h = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, res, num_threads=16)
+    t1 = time.perf_counter()
+    d = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, res, device=0)
+    t2 = time.perf_counter()
+    print(f"{name} {res}: host {1e3 * (t1 - t0):.1f} ms, device {1e3 * (t2 - t1):.1f} ms, "
+          f"{h.num_refs} refs")
+    assert bytes(h.scene.grid) == bytes(d.scene.grid)
+    assert h.num_refs == d.num_refs
+    assert np.array_equal(h.cells(), d.cells())
+    assert np.array_equal(h.indices(), d.indices())
+    assert np.array_equal(h.tri_pos().view(np.uint32), d.tri_pos().view(np.uint32))
+    assert np.array_equal(h.tri_data().view(np.uint32), d.tri_data().view(np.uint32))
+    assert np.array_equal(h.tri_material(), d.tri_material())
+
+
+def test_device_build_rejects_bad_args():
+    soup = scenes.get_scene("sphere")
+    with pytest.raises(native.ZrtError):
+        native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, (0, 128, 128), device=0)
+    with pytest.raises(native.ZrtError):
+        native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, (8, 8, 8), device=99)

@@ -200,8 +200,12 @@ int main(int argc, char** argv) {
         const auto t = Clock::now();
         info("Grid resolution: { " + std::to_string(cfg.res[0]) + ", " + std::to_string(cfg.res[1]) + ", " +
              std::to_string(cfg.res[2]) + " }");
-        if ((rc = zrt_geometry_build(pos, nrm, uv, mat, ntri, cfg.res, num_threads, &geo)) != ZRT_OK)
-            return fail("Geometry.build", rc);
+        // on the first render GPU (grid_build.hip); ZRT_HOST_BUILD=1: host threads.
+        // Both give the same arrays bit for bit.
+        const char* hb = getenv("ZRT_HOST_BUILD");
+        rc = (hb && atoi(hb) != 0) ? zrt_geometry_build(pos, nrm, uv, mat, ntri, cfg.res, num_threads, &geo)
+                                   : zrt_geometry_build_device(pos, nrm, uv, mat, ntri, cfg.res, devices[0], &geo);
+        if (rc != ZRT_OK) return fail("Geometry.build", rc);
         zrt_geometry_scene(geo, &scene);
         uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0;
         for (uint32_t c = 0; c < scene.num_cells; ++c) {

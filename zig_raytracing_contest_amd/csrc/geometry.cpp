@@ -17,19 +17,9 @@
 #include <thread>
 #include <vector>
 
-#include "zrt_internal.h"
+#include "geometry.h"
 
 using namespace zrt;
-
-struct zrt_geometry {
-    Grid grid;
-    uint32_t ncells = 0;
-    std::vector<uint32_t> cells;     // 2*ncells {begin, end}
-    std::vector<uint32_t> indices;   // refs -> source triangle
-    std::vector<float> pos;          // refs*9 : v0, e1, e2
-    std::vector<float> data;         // refs*15
-    std::vector<uint32_t> mat;       // refs
-};
 
 namespace {
 
@@ -70,22 +60,13 @@ extern "C" int zrt_geometry_build(const float* positions, const float* normals,
                                   uint32_t num_threads, zrt_geometry** out) {
     if (!out) return ZRT_ERR_INVALID_ARG;
     *out = nullptr;
-    if (!positions || !normals || !texcoords || !material || !resolution || n == 0)
-        return ZRT_ERR_INVALID_ARG;
+    const int arc = check_build_args(positions, normals, texcoords, material, n, resolution);
+    if (arc != ZRT_OK) return arc;
     const uint64_t ncells64 = (uint64_t)resolution[0] * resolution[1] * resolution[2];
-    if (resolution[0] == 0 || resolution[1] == 0 || resolution[2] == 0 || ncells64 > 0x7FFFFFFFull)
-        return ZRT_ERR_INVALID_ARG;
     zrt_geometry* geo = new (std::nothrow) zrt_geometry();
     if (!geo) return ZRT_ERR_OUT_OF_MEMORY;
     try {
-        // stage2.zig:44-57 initGrid (sequential, same min/max order)
-        Bbox bb{mk(kInf, kInf, kInf), mk(-kInf, -kInf, -kInf)};
-        for (uint64_t i = 0; i < 3ull * n; ++i) {
-            const v3 p = ld3(positions + 3 * i);
-            bb.min = vmin(bb.min, p);
-            bb.max = vmax(bb.max, p);
-        }
-        geo->grid = grid_init(bb, resolution);
+        geo->grid = scene_grid(positions, n, resolution);   // stage2.zig:44-57
         geo->ncells = (uint32_t)ncells64;
 
         // SAT binning on host threads (stage2.zig:59-79 / 104-124)

@@ -87,6 +87,7 @@ class Outputs(C.Structure):
 
 EXPORTS = [
     "zrt_error_string", "zrt_abi_version", "zrt_device_count", "zrt_geometry_build",
+    "zrt_geometry_build_device",
     "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
     "zrt_context_create", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
     "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
@@ -107,6 +108,8 @@ def lib():
     L.zrt_device_count.argtypes = [C.POINTER(C.c_int)]
     L.zrt_geometry_build.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_void_p)]
+    L.zrt_geometry_build_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                            C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_void_p)]
     L.zrt_geometry_scene.argtypes = [C.c_void_p, C.POINTER(Scene)]
     L.zrt_geometry_indices.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint32)),
                                        C.POINTER(C.c_uint32)]
@@ -174,17 +177,21 @@ def tile_pixels(w, h, tile=64, rank=0, num_ranks=1) -> np.ndarray:
 
 
 class Geometry:
-    """stage2.Geometry: build (SAT binning) + bake, on host threads."""
+    """stage2.Geometry: build (SAT binning) + bake, on host threads, or on
+    GPU `device` (zrt_geometry_build_device: same arrays, bit for bit)."""
 
-    def __init__(self, pos, nrm, uv, mat, resolution=(128, 128, 128), num_threads=0):
+    def __init__(self, pos, nrm, uv, mat, resolution=(128, 128, 128), num_threads=0, device=None):
         self._keep = [np.ascontiguousarray(pos, np.float32), np.ascontiguousarray(nrm, np.float32),
                       np.ascontiguousarray(uv, np.float32), np.ascontiguousarray(mat, np.uint32)]
         n = self._keep[3].size
         res = (C.c_uint32 * 3)(*resolution)
         h = C.c_void_p()
-        check(lib().zrt_geometry_build(self._keep[0].ctypes.data, self._keep[1].ctypes.data,
-                                       self._keep[2].ctypes.data, self._keep[3].ctypes.data, n,
-                                       res, num_threads, C.byref(h)), "zrt_geometry_build")
+        args = [k.ctypes.data for k in self._keep] + [n, res]
+        if device is None:
+            check(lib().zrt_geometry_build(*args, num_threads, C.byref(h)), "zrt_geometry_build")
+        else:
+            check(lib().zrt_geometry_build_device(*args, int(device), C.byref(h)),
+                  "zrt_geometry_build_device")
         self._h = h
         self.scene = Scene()
         check(lib().zrt_geometry_scene(self._h, C.byref(self.scene)), "zrt_geometry_scene")
@@ -210,6 +217,12 @@ class Geometry:
 
     def tri_pos(self):
         return np.ctypeslib.as_array(self.scene.triangles_pos, (self.num_refs, 9)).copy()
+
+    def tri_data(self):
+        return np.ctypeslib.as_array(self.scene.triangles_data, (self.num_refs, 15)).copy()
+
+    def tri_material(self):
+        return np.ctypeslib.as_array(self.scene.triangles_material, (self.num_refs,)).copy()
 
 
 def attach_materials(scene: Scene, tex_desc: np.ndarray, texels: np.ndarray, keep: list):
