@@ -100,3 +100,23 @@ def test_render_needs_gpu_and_fails_loudly():
     with pytest.raises(native.ZrtError) as e:
         native.Context(g.scene)
     assert e.value.status == -2
+
+
+@pytest.mark.parametrize("w,h", [(1920, 1080), (7, 3), (1, 1), (640, 2000)])
+def test_png_write_parallel_deflate_roundtrip(tmp_path, w, h):
+    """zrt_png_write (main.zig:129-140 stbi_write_png stand-in): the zlib
+    stream is deflated in row pieces on host threads and must still decode,
+    pixel for pixel, with an independent reader."""
+    import ctypes as C
+    from zig_raytracing_contest_amd import pngio
+    rng = np.random.default_rng(w * 7 + h)
+    y, x = np.mgrid[0:h, 0:w]
+    img = np.stack([(x * 255 // max(w - 1, 1)), (y * 255 // max(h - 1, 1)),
+                    rng.integers(0, 256, (h, w))], -1).astype(np.uint8)
+    p = str(tmp_path / "o.png")
+    L = native.lib()
+    L.zrt_png_write.argtypes = [C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]
+    assert L.zrt_png_write(p.encode(), img.ctypes.data, w, h) == 0
+    got = pngio.read(p)
+    assert got.shape[:2] == (h, w)
+    assert np.array_equal(got[..., :3], img)

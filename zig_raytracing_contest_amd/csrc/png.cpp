@@ -14,6 +14,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <thread>
+#include <vector>
 
 #include "zrt_internal.h"
 
@@ -222,9 +225,54 @@ int png_encode_rgb(const uint8_t* rgb, int w, int h, int level, std::vector<uint
         const uint8_t* src = rgb + (size_t)y * rb;
         for (size_t i = 0; i < rb; ++i) line[1 + i] = (uint8_t)(src[i] - (i >= 3 ? src[i - 3] : 0));
     }
-    uLongf zn = compressBound((uLong)raw.size());
-    std::vector<uint8_t> z(zn);
-    if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), level) != Z_OK) return ZRT_ERR_IO;
+    // zlib stream deflated in parallel: row-aligned pieces,
+    // each a raw deflate ended by a sync flush (byte-aligned, non-final
+    // blocks) except the last, concatenated behind one zlib header; the
+    // Adler-32 of the whole is combined from the pieces'.  A valid single
+    // stream: any inflater (and stbi) reads it; only the file bytes differ
+    // from a one-thread deflate (each piece starts with an empty window).
+    const size_t row = rb + 1;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t min_piece = 256 * 1024;
+    size_t np = std::min<size_t>(std::min<size_t>(hw, 32), std::max<size_t>(1, raw.size() / min_piece));
+    np = std::min<size_t>(np, (size_t)h);
+    std::vector<std::vector<uint8_t>> zp(np);
+    std::vector<uLong> ad(np, 0);
+    std::vector<size_t> beg(np + 1);
+    for (size_t k = 0; k <= np; ++k) beg[k] = (size_t)h * k / np * row;
+    std::vector<int> ok(np, 0);
+    auto piece = [&](size_t k) {
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return;
+        const size_t len = beg[k + 1] - beg[k];
+        zp[k].resize(deflateBound(&zs, (uLong)len) + 16);
+        zs.next_in = raw.data() + beg[k];
+        zs.avail_in = (uInt)len;
+        zs.next_out = zp[k].data();
+        zs.avail_out = (uInt)zp[k].size();
+        const int r = deflate(&zs, k + 1 == np ? Z_FINISH : Z_SYNC_FLUSH);
+        const bool done = k + 1 == np ? r == Z_STREAM_END : (r == Z_OK && zs.avail_in == 0);
+        zp[k].resize(zs.total_out);
+        deflateEnd(&zs);
+        ad[k] = adler32(adler32(0L, Z_NULL, 0), raw.data() + beg[k], (uInt)len);
+        ok[k] = done ? 1 : 0;
+    };
+    {
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < np; ++k) th.emplace_back(piece, k);
+        piece(0);
+        for (auto& t : th) t.join();
+    }
+    std::vector<uint8_t> z = {0x78, 0x9C};   // CM 8, 32K window; FCHECK valid
+    uLong adl = adler32(0L, Z_NULL, 0);
+    for (size_t k = 0; k < np; ++k) {
+        if (!ok[k]) return ZRT_ERR_IO;
+        z.insert(z.end(), zp[k].begin(), zp[k].end());
+        adl = adler32_combine(adl, ad[k], (z_off_t)(beg[k + 1] - beg[k]));
+    }
+    for (int sh = 24; sh >= 0; sh -= 8) z.push_back((uint8_t)(adl >> sh));
+    const size_t zn = z.size();
     out->clear();
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     out->insert(out->end(), sig, sig + 8);
