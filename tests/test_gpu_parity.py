@@ -183,6 +183,32 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
         tuple(int(x) for x in ctr[:4])
 
 
+# The timed kernels (no counting build) against the oracle on every scene:
+# the default wavefront path (XCD-split primary launch), without the split,
+# with region queues on every launch, the split and the megakernel.
+MODES = [("wf", {}), ("wf", {"ZRT_XCD": "0"}), ("wf", {"ZRT_XCD": "2"}), ("split", {}), ("mega", {})]
+
+
+@pytest.mark.parametrize("mode,env", MODES, ids=lambda m: str(m))
+@pytest.mark.parametrize("name,camname,w,h,spp", CASES)
+def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mode, env, name, camname,
+                                         w, h, spp):
+    monkeypatch.setenv("ZRT_MODE", mode)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    soup = scenes.get_scene(name)
+    c = soup.camera(camname)
+    aspect = c.aspect
+    cam = camera_for(soup, camname, None if aspect else w, h)
+    img, res = gpu_scenes(name).render(cam, num_samples=spp, max_bounce=4, linear=True)
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, aspect, None if aspect else w, h)
+    rgb, lin, ctr = oracle_mod.OracleScene(soup).render(ocam, spp, 4, oracle_mod.RNG_PATH, 0, 16)
+    pix = native.tile_pixels(cam.w, cam.h)
+    assert np.array_equal(res["linear"], lin[pix])
+    assert np.array_equal(img.reshape(-1, 3), rgb)
+    assert res["stats"]["segments"] == int(ctr[0])
+
+
 # per-item pass bytes of each kernel organisation (render.hip: per_item)
 PER_ITEM = {"mega": 16, "wf": 96 + 16 + 32 * 4, "split": 96 + 16 + 16 + 32 * 4}
 

@@ -537,7 +537,19 @@ struct WfParams {
     uint32_t refill;          // split mode: idle lanes before a wave fetches rays
     uint32_t* hist;           // ray sort: per-key counts of the appended paths (null: no sort)
     uint32_t sort_bits;       // ray sort: origin-region bits per axis
+    // XCD split (wf_kernel): 8 block groups, one per XCD; the queue is cut into
+    // 8 regions, region g holding the paths of pixel range g (capacity S*Pg)
+    uint32_t xcd;             // 0: one queue, one counter
+    uint32_t* fetch8;         // work counter per group of this launch
+    const uint32_t* n_in8;    // paths per region of q_in
+    uint32_t* n_out8;         // paths per region of q_out
 };
+
+// XCD split: first pixel (packed order) of group g, 8x8-block aligned.
+__device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
+    const uint32_t nblk = (P + 63u) >> 6;
+    return min(P, (nblk * g / 8u) * 64u);
+}
 
 // Ray-sort key of a continuing path: the origin's region in a 2^R per axis
 // subdivision of the grid bbox (Morton order), then the direction octant.
@@ -630,12 +642,31 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
 }
 
 // Append the wave's continuing paths to the next queue: one returning atomic
-// per wave, ranks from ballot + popcount.
+// per wave, ranks from ballot + popcount.  XCD split: to the region of the
+// wave's pixel group `reg` (all 64 items of a fetch come from one region).
 __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d,
                                          uint32_t item, uint32_t depth, uint32_t slot, const Rng& rng,
-                                         uint32_t mask) {
+                                         uint32_t mask, uint32_t reg = 0) {
     const uint64_t bal = __ballot(cont);
     if (!bal) return;
+    if (w.n_out8) {
+        const uint32_t S = w.t.total / max(w.t.P, 1u);
+        uint32_t ob = 0;
+        if ((threadIdx.x & 63u) == 0) {
+            ob = atomicAdd(&w.n_out8[reg], (uint32_t)__popcll(bal));
+            atomicAdd(w.n_out, (uint32_t)__popcll(bal));         // total (debug counts)
+        }
+        ob = __builtin_amdgcn_readfirstlane(ob) + S * xcd_q0(w.t.P, reg);
+        if (cont) {
+            const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
+            w.q_out[3ull * pos] = make_float4(o.x, o.y, o.z, __uint_as_float(item));
+            w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
+            w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s),
+                                                  __uint_as_float((uint32_t)(rng.s >> 32)),
+                                                  __uint_as_float(mask), 0.0f);
+        }
+        return;
+    }
     uint32_t key = 0;
     if (w.hist) {
         key = cont ? sort_key(w.t, o, d, w.sort_bits) : 0u;
@@ -669,19 +700,47 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const uint32_t n = PRIMARY ? p.total : *w.n_in;
     uint32_t n_seg = 0, dummy = 0;
     uint64_t prof_dummy[11];
+    // XCD split (w.xcd): blocks are dispatched round-robin over the 8 XCDs,
+    // so group g = blockIdx % 8 shares one L2.  Group g takes pixel range g
+    // (8x8-block aligned) for every sample of the pass, and in later bounces
+    // the queue region of those pixels' paths, then helps the other groups:
+    // a screen region's paths stay on one XCD from bounce to bounce.  Same
+    // items, other order: same image.
+    uint32_t grp = blockIdx.x & 7u, tried = 0;
+    const uint32_t S = p.total / max(p.P, 1u);
 
     for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(w.fetch, 64u);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= n) break;
-        const uint32_t i = base + lane;
+        uint32_t base = 0, i = 0, reg = 0;
+        bool valid;
+        if (w.xcd) {
+            uint32_t q0 = 0, pg = 0, lim = 0;
+            for (;;) {
+                q0 = xcd_q0(p.P, grp);
+                pg = xcd_q0(p.P, grp + 1u) - q0;
+                lim = PRIMARY ? S * pg : w.n_in8[grp];
+                if (lane == 0) base = atomicAdd(&w.fetch8[grp], 64u);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (base < lim || ++tried == 8u) break;
+                grp = (grp + 1u) & 7u;
+            }
+            if (tried == 8u) break;
+            reg = grp;
+            const uint32_t j = base + lane;
+            valid = j < lim;
+            i = !valid ? 0u : PRIMARY ? (j / pg) * p.P + q0 + j % pg : S * q0 + j;
+        } else {
+            if (lane == 0) base = atomicAdd(w.fetch, 64u);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (base >= n) break;
+            i = base + lane;
+            valid = i < n;
+        }
         bool cont = false;
         uint32_t mask = 0, r_item = 0, r_depth = 0, r_slot = 0;
         v3 r_o = mk(0, 0, 0), r_d = mk(0, 0, 0);
         Rng r_rng;
         r_rng.s = 0;
-        if (i < n) {
+        if (valid) {
             uint32_t item, depth, slot;
             Rng rng;
             v3 o, d;
@@ -712,7 +771,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
         }
-        wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask);
+        wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask, reg);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -1395,7 +1454,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * std::max<uint32_t>(mb, 1))) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 2ull * (mb + 2))) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 18ull * (mb + 2))) != ZRT_OK) return rc;
         if (split && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
@@ -1473,10 +1532,15 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         return rc;
     }
     uint32_t refill = 48;
+    // XCD-aware split of the wavefront launches (wf_kernel): ZRT_XCD=0/1/2,
+    // default 1 (primary launch only: cfg3 64 spp 1967 vs 1834 Mrays/s)
+    uint32_t xcd_mode = 1;
+    if (const char* e = getenv("ZRT_XCD")) xcd_mode = (uint32_t)std::max(0, std::min(2, atoi(e)));
     // ray sort between bounces (ZRT_SORT = origin-region bits per axis, 0 = off)
     uint32_t sort_bits = 0;
     if (const char* e = getenv("ZRT_SORT")) sort_bits = (uint32_t)std::max(0, std::min(4, atoi(e)));
     const bool sorting = wf && sort_bits > 0 && mb > 1;
+    if (!(wf && !split && !wave_mode && !sorting)) xcd_mode = 0;   // wf_kernel only
     const uint32_t nbins = 8u << (3 * sort_bits);
     if (sorting) {
         if ((rc = grow(&c->d_hist, &c->hist_cap, nbins)) != ZRT_OK) return rc;
@@ -1530,7 +1594,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
         if (wf) {
             // counters: n[k] = live paths entering bounce k, fetch[k] = work counter of launch k
-            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 8ull * (mb + 2), c->stream));
+            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 18 * (mb + 2), c->stream));
             uint32_t* n = c->d_wfc;
             uint32_t* fetch = c->d_wfc + (mb + 2);
             WfParams W;
@@ -1556,6 +1620,14 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.n_in = n + k;
                 W.n_out = n + k + 1;
                 W.fetch = fetch + k;
+                // XCD split: per launch k, 8 work counters + 8 region counts (entering k)
+                uint32_t* x8 = c->d_wfc + 2 * (mb + 2);
+                // 1: the primary launch only (its appends go to the one queue);
+                // 2: every launch, with region queues (r01: bounces 2.4x slower)
+                W.xcd = (xcd_mode == 2 || (xcd_mode == 1 && k == 0)) ? 1u : 0u;
+                W.fetch8 = x8 + 16 * k;
+                W.n_in8 = x8 + 16 * k + 8;
+                W.n_out8 = xcd_mode == 2 ? x8 + 16 * (k + 1) + 8 : nullptr;
                 if (!split || mb > 0) {
                     HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
                     if (k == 0)
