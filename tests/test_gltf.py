@@ -104,3 +104,49 @@ def test_load_errors(tmp_path):
     with pytest.raises(native.ZrtError) as e:
         native.Gltf(str(bad))
     assert e.value.status == -7
+
+
+def _texels_to_u8(lin):
+    """Invert the loader's per-byte sRGB->linear map (scenes.srgb8_to_linear)."""
+    lut = scenes.srgb8_to_linear(np.arange(256, dtype=np.uint8))
+    idx = np.searchsorted(lut, lin)
+    idx = np.clip(idx, 0, 255)
+    assert np.array_equal(lut[idx], lin)
+    return idx.astype(np.int32)
+
+
+@pytest.mark.parametrize("w,h,mode,kw", [
+    (37, 23, "RGB", dict(quality=90, subsampling=0)),                    # baseline 4:4:4
+    (64, 48, "RGB", dict(quality=75, subsampling=2)),                    # 4:2:0
+    (33, 17, "RGB", dict(quality=85, subsampling=1)),                    # 4:2:2, odd size
+    (50, 41, "RGB", dict(quality=80, subsampling=2, progressive=True)),  # progressive
+    (40, 40, "RGB", dict(quality=95, subsampling=0, progressive=True)),
+    (29, 31, "L", dict(quality=90)),                                     # grayscale
+    (48, 32, "RGB", dict(quality=70, subsampling=2, restart_marker_blocks=2)),   # DRI
+])
+def test_jpeg_texture_decode(tmp_path, w, h, mode, kw):
+    """JPEG textures (stage1.zig:58 stbi_loadf_from_memory on a JPEG; SURVEY.md
+    §8 f1): the loader's decode against an independent decoder (PIL/libjpeg)
+    on PIL-encoded images.  stb_image itself is not in the reference tree,
+    so these texels are parity unpinned; the bar is a small per-channel
+    tolerance (different IDCT rounding / upsampling filters)."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(w * h)
+    y, x = np.mgrid[0:h, 0:w]
+    base = np.stack([x * 255 // w, y * 255 // h, (x + y) * 127 // (w + h) + 60], -1)
+    img = np.clip(base + rng.integers(-20, 21, base.shape), 0, 255).astype(np.uint8)
+    pil = Image.fromarray(img if mode == "RGB" else img[..., 0], mode)
+    p = tmp_path / "t.jpg"
+    pil.save(str(p), "JPEG", **kw)
+    ref = np.asarray(Image.open(str(p)).convert("RGB")).astype(np.int32)
+    doc = {"asset": {"version": "2.0"}, "images": [{"uri": p.name}],
+           "textures": [{"source": 0}], "materials": [
+               {"pbrMetallicRoughness": {"baseColorTexture": {"index": 0}}}]}
+    gp = tmp_path / "t.gltf"
+    gp.write_text(json.dumps(doc))
+    desc, tex = native.Gltf(str(gp)).materials()
+    assert (desc[0, 0, 1], desc[0, 0, 2]) == (w, h)
+    got = _texels_to_u8(tex[desc[0, 0, 0]:desc[0, 0, 0] + w * h * 3].reshape(h, w, 3))
+    d = np.abs(got - ref)
+    assert d.max() <= 3, (d.max(), d.mean())
+    assert d.mean() < 0.5, d.mean()

@@ -17,7 +17,7 @@
 // non-indexed primitives, and an error for a primitive without material.
 // zgltf's TRS composition and matrix product order are not recoverable
 // offline (submodule empty): "parity unpinned" for node transforms that are
-// not identity.  Images: PNG (own decoder); JPEG -> unsupported.
+// not identity.  Images: PNG (png.cpp) and JPEG (jpeg.cpp) decoders.
 #include <array>
 #include <cmath>
 #include <memory>
@@ -258,8 +258,8 @@ int load_images(Loader& L, uint32_t nthreads, std::vector<Image8>* images) {
                 data = bytes.data();
                 len = bytes.size();
             }
-            if (len >= 2 && data[0] == 0xFF && data[1] == 0xD8) { rc[i] = ZRT_ERR_UNSUPPORTED; continue; }
-            rc[i] = png_decode(data, len, &(*images)[i]);
+            rc[i] = (len >= 2 && data[0] == 0xFF && data[1] == 0xD8) ? jpeg_decode(data, len, &(*images)[i])
+                                                                      : png_decode(data, len, &(*images)[i]);
         }
     };
     const size_t nt = std::max<size_t>(1, std::min<size_t>(nthreads ? nthreads : std::thread::hardware_concurrency(), n));

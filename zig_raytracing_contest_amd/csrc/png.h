@@ -17,6 +17,8 @@ struct Image8 {
 };
 
 int png_decode(const uint8_t* data, size_t n, Image8* out);
+// JPEG (jpeg.cpp): baseline/extended/progressive Huffman, 8-bit, Gray or YCbCr -> RGBA8
+int jpeg_decode(const uint8_t* data, size_t n, Image8* out);
 int png_encode_rgb(const uint8_t* rgb, int w, int h, int level, std::vector<uint8_t>* out);
 int png_write_rgb(const char* path, const uint8_t* rgb, int w, int h, int level);
 
