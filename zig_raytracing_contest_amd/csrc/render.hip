@@ -602,6 +602,17 @@ __device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, 
                       scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
 }
 
+// The RNG state camera_ray leaves (after the jitter draws), without the ray.
+__device__ __forceinline__ Rng camera_rng(const TraceParams& p, uint32_t item) {
+    const uint32_t s_local = item / p.P;
+    const uint32_t pixel = p.pixlist[item - s_local * p.P];
+    Rng rng;
+    rng.s = path_key(p.seed, pixel, p.s0 + s_local);
+    (void)rng_float(rng);
+    (void)rng_float(rng);
+    return rng;
+}
+
 // traceRayRecursive's body after the hit (stage3.zig:195-219) for one
 // segment: env colour on a miss, else material lookup, (e, a) pair to the
 // bounce stack on a scatter, pass-through otherwise.  Returns true when the
@@ -699,7 +710,6 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
     const uint32_t n = PRIMARY ? p.total : *w.n_in;
     uint32_t n_seg = 0, dummy = 0;
-    uint64_t prof_dummy[11];
     // XCD split (w.xcd): blocks are dispatched round-robin over the 8 XCDs,
     // so group g = blockIdx % 8 shares one L2.  Group g takes pixel range g
     // (8x8-block aligned) for every sample of the pass, and in later bounces
@@ -741,20 +751,33 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
         Rng r_rng;
         r_rng.s = 0;
         if (valid) {
-            uint32_t item, depth, slot;
-            Rng rng;
+            // the ray only: the rest of the path's state (item, slot, RNG,
+            // mask) is re-read after the walk, so it holds no VGPRs in it
             v3 o, d;
+            uint32_t depth;
             if (PRIMARY) {
-                item = i;
-                camera_ray(p, item, rng, o, d);
+                Rng rng0;
+                camera_ray(p, i, rng0, o, d);
                 depth = p.max_bounce;
-                slot = 0;
             } else {
-                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1];
                 o = mk(a.x, a.y, a.z);
-                item = __float_as_uint(a.w);
                 d = mk(b.x, b.y, b.z);
                 depth = __float_as_uint(b.w) & 0xFFFFu;
+            }
+            float t = kInf, hu = 0.0f, hv = 0.0f;
+            uint32_t hidx = 0;
+            if (depth != 0)
+                t = trace_ray<false, false, TB, MB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
+            uint32_t item, slot;
+            Rng rng;
+            if (PRIMARY) {
+                item = i;
+                slot = 0;
+                rng = camera_rng(p, i);
+            } else {
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                item = __float_as_uint(a.w);
                 slot = __float_as_uint(b.w) >> 16;
                 rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
                 mask = __float_as_uint(c.z);
@@ -762,10 +785,6 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             v3 L = mk(0, 0, 0);
             if (depth != 0) {
                 ++n_seg;
-                float hu = 0.0f, hv = 0.0f;
-                uint32_t hidx = 0;
-                const float t = trace_ray<false, false, TB, MB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy,
-                                                                prof_dummy);
                 cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
             }
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
