@@ -126,6 +126,10 @@ typedef struct zrt_stats {
 const char* zrt_error_string(int status);
 int zrt_abi_version(void);
 int zrt_device_count(int* count);
+/* Optional: create the device's context and load the library's kernels now
+ * (otherwise the first GPU call pays ~0.1-0.2 s), e.g. on a thread while the
+ * host loads the scene.  device -1 = 0. */
+int zrt_device_warmup(int device);
 
 /* ---- stage 2: grid build + bake (stage2.zig:44-164) --------------------- */
 typedef struct zrt_geometry zrt_geometry;

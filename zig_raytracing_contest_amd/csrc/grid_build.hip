@@ -294,6 +294,13 @@ int build_on_device(const float* positions, const float* normals, const float* t
 
 }  // namespace
 
+// Load this translation unit's code objects (its own module: the scans and
+// sorts) on the current device; called by zrt_device_warmup.
+int grid_build_warmup() {
+    hipFuncAttributes fa;
+    return hipFuncGetAttributes(&fa, (const void*)cand_kernel) == hipSuccess ? ZRT_OK : ZRT_ERR_HIP;
+}
+
 extern "C" int zrt_geometry_build_device(const float* positions, const float* normals, const float* texcoords,
                                          const uint32_t* material, uint32_t n, const uint32_t resolution[3],
                                          int device, zrt_geometry** out) {

@@ -1182,6 +1182,7 @@ struct zrt_context {
     std::vector<hipEvent_t> ev_trace;
     zrt_grid grid{};
     uint32_t ncells = 0, nrefs = 0, nmat = 0;
+    bool has_ids = false;            // tri_pos w holds shape ids (ZRT_MB=1 at creation)
     uint2* d_cells = nullptr;
     float4* d_pos = nullptr;
     float4* d_data = nullptr;
@@ -1240,6 +1241,8 @@ static int validate_scene(const zrt_scene* s) {
     return ZRT_OK;
 }
 
+int grid_build_warmup();   // grid_build.hip
+
 extern "C" int zrt_device_count(int* count) {
     if (!count) return ZRT_ERR_INVALID_ARG;
     *count = 0;
@@ -1247,6 +1250,21 @@ extern "C" int zrt_device_count(int* count) {
     if (hipGetDeviceCount(&n) != hipSuccess) return ZRT_ERR_NO_DEVICE;
     *count = n;
     return ZRT_OK;
+}
+
+// Start-up work of the first GPU call, done ahead: the device's context and
+// the library's code objects (one fat binary, loaded on first use: ~0.1-0.2 s
+// on MI355X).  Lets a host overlap it with file loading.
+extern "C" int zrt_device_warmup(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
+    if (device < 0) device = 0;
+    if (device >= n) return ZRT_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    HIP_TRY(hipFree(nullptr));
+    hipFuncAttributes fa;
+    HIP_TRY(hipFuncGetAttributes(&fa, (const void*)resolve_kernel));
+    return grid_build_warmup();
 }
 
 extern "C" void zrt_context_destroy(zrt_context* c) {
@@ -1301,7 +1319,11 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
     std::vector<float4> pos(3 * nr), dat(4 * nr);
-    const std::vector<uint32_t> shape = shape_ids(s->triangles_pos, c->nrefs);
+    // shape ids (tri_pos w) only for the opt-in mailbox variant: the hash over
+    // every ref costs tens of ms of context creation (the CLI's wall clock)
+    c->has_ids = getenv("ZRT_MB") && atoi(getenv("ZRT_MB")) == 1;
+    const std::vector<uint32_t> shape = c->has_ids ? shape_ids(s->triangles_pos, c->nrefs)
+                                                   : std::vector<uint32_t>(c->nrefs, 0u);
     for (uint32_t i = 0; i < c->nrefs; ++i) {
         const float* q = s->triangles_pos + 9ull * i;
         float idf;
@@ -1521,7 +1543,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         case 7: ZRT_WF_PICK(K, 7); break;                                    \
         default: ZRT_WF_PICK(K, 8); break;                                   \
     }
-        const char* mbe = getenv("ZRT_MB");
+        const char* mbe = c->has_ids ? getenv("ZRT_MB") : nullptr;   // needs the ids
         const char* tbe = getenv("ZRT_TB");      // tuning sweeps only
         const int tbv = tbe ? atoi(tbe) : kTriBatch;
         if (!wave_mode && !split && tbv != kTriBatch && (tbv == 1 || tbv == 3 || tbv == 4)) {

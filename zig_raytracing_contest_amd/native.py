@@ -86,7 +86,7 @@ class Outputs(C.Structure):
 
 
 EXPORTS = [
-    "zrt_error_string", "zrt_abi_version", "zrt_device_count", "zrt_geometry_build",
+    "zrt_error_string", "zrt_abi_version", "zrt_device_count", "zrt_device_warmup", "zrt_geometry_build",
     "zrt_geometry_build_device",
     "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
     "zrt_context_create", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
