@@ -184,9 +184,11 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 
 
 # The timed kernels (no counting build) against the oracle on every scene:
-# the default wavefront path (XCD-split primary launch), without the split,
-# with region queues on every launch, the split and the megakernel.
-MODES = [("wf", {}), ("wf", {"ZRT_XCD": "0"}), ("wf", {"ZRT_XCD": "2"}), ("split", {}), ("mega", {})]
+# the default wavefront path (XCD split with region queues), without the
+# split, with the split on the primary launch only, with packed counters, the
+# split organisation and the megakernel.
+MODES = [("wf", {}), ("wf", {"ZRT_XCD": "0"}), ("wf", {"ZRT_XCD": "1"}), ("wf", {"ZRT_CTR": "1"}),
+         ("split", {}), ("mega", {})]
 
 
 @pytest.mark.parametrize("mode,env", MODES, ids=lambda m: str(m))

@@ -541,9 +541,14 @@ struct WfParams {
     // 8 regions, region g holding the paths of pixel range g (capacity S*Pg)
     uint32_t xcd;             // 0: one queue, one counter
     uint32_t* fetch8;         // work counter per group of this launch
+    uint32_t ctr;             // region counter stride (u32)
     const uint32_t* n_in8;    // paths per region of q_in
     uint32_t* n_out8;         // paths per region of q_out
 };
+
+// Work / append counters: `ctr` u32 apart (32: one per 128-byte line, so the
+// waves' atomics on different counters do not queue on one line; 1: packed).
+constexpr uint32_t kCtrMax = 32;
 
 // XCD split: first pixel (packed order) of group g, 8x8-block aligned.
 __device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
@@ -663,10 +668,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
     if (w.n_out8) {
         const uint32_t S = w.t.total / max(w.t.P, 1u);
         uint32_t ob = 0;
-        if ((threadIdx.x & 63u) == 0) {
-            ob = atomicAdd(&w.n_out8[reg], (uint32_t)__popcll(bal));
-            atomicAdd(w.n_out, (uint32_t)__popcll(bal));         // total (debug counts)
-        }
+        if ((threadIdx.x & 63u) == 0) ob = atomicAdd(&w.n_out8[reg * w.ctr], (uint32_t)__popcll(bal));
         ob = __builtin_amdgcn_readfirstlane(ob) + S * xcd_q0(w.t.P, reg);
         if (cont) {
             const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
@@ -727,8 +729,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             for (;;) {
                 q0 = xcd_q0(p.P, grp);
                 pg = xcd_q0(p.P, grp + 1u) - q0;
-                lim = PRIMARY ? S * pg : w.n_in8[grp];
-                if (lane == 0) base = atomicAdd(&w.fetch8[grp], 64u);
+                lim = PRIMARY ? S * pg : w.n_in8[grp * w.ctr];
+                if (lane == 0) base = atomicAdd(&w.fetch8[grp * w.ctr], 64u);
                 base = __builtin_amdgcn_readfirstlane(base);
                 if (base < lim || ++tried == 8u) break;
                 grp = (grp + 1u) & 7u;
@@ -1495,7 +1497,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * std::max<uint32_t>(mb, 1))) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 18ull * (mb + 2))) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 18ull * kCtrMax * (mb + 2))) != ZRT_OK) return rc;
         if (split && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
@@ -1574,9 +1576,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
     uint32_t refill = 48;
     // XCD-aware split of the wavefront launches (wf_kernel): ZRT_XCD=0/1/2,
-    // default 1 (primary launch only: cfg3 64 spp 1967 vs 1834 Mrays/s)
-    uint32_t xcd_mode = 1;
+    // default 2 (cfg3 64 spp, one process: 1902 vs 1855 for 1 vs 1767 for 0)
+    uint32_t xcd_mode = 2;
+    uint32_t ctr_stride = 32;   // counter stride in u32 (ZRT_CTR=1: packed)
+    if (const char* e = getenv("ZRT_CTR")) ctr_stride = atoi(e) == 1 ? 1u : 32u;
     if (const char* e = getenv("ZRT_XCD")) xcd_mode = (uint32_t)std::max(0, std::min(2, atoi(e)));
+    // (the counter stride is what made mode 2 pay: packed, its 8+8 region
+    // counters shared lines with the others and it ran 1091 vs 1902)
     // ray sort between bounces (ZRT_SORT = origin-region bits per axis, 0 = off)
     uint32_t sort_bits = 0;
     if (const char* e = getenv("ZRT_SORT")) sort_bits = (uint32_t)std::max(0, std::min(4, atoi(e)));
@@ -1635,9 +1641,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
         if (wf) {
             // counters: n[k] = live paths entering bounce k, fetch[k] = work counter of launch k
-            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 18 * (mb + 2), c->stream));
-            uint32_t* n = c->d_wfc;
-            uint32_t* fetch = c->d_wfc + (mb + 2);
+            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 18 * kCtrMax * (mb + 2), c->stream));
+            const uint32_t kCtr = ctr_stride;
+            uint32_t* n = c->d_wfc;                       // n[k * kCtr]
+            uint32_t* fetch = c->d_wfc + kCtr * (mb + 2);  // fetch[k * kCtr]
             WfParams W;
             W.t = tp;
             W.stk = c->d_stk;
@@ -1658,17 +1665,18 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 }
                 const bool sort_out = sorting && k + 1 < nb;
                 W.hist = sort_out ? c->d_hist : nullptr;
-                W.n_in = n + k;
-                W.n_out = n + k + 1;
-                W.fetch = fetch + k;
+                W.n_in = n + kCtr * k;
+                W.n_out = n + kCtr * (k + 1);
+                W.fetch = fetch + kCtr * k;
                 // XCD split: per launch k, 8 work counters + 8 region counts (entering k)
-                uint32_t* x8 = c->d_wfc + 2 * (mb + 2);
+                uint32_t* x8 = c->d_wfc + 2 * kCtr * (mb + 2);
                 // 1: the primary launch only (its appends go to the one queue);
-                // 2: every launch, with region queues (r01: bounces 2.4x slower)
+                // 2: every launch, with region queues
                 W.xcd = (xcd_mode == 2 || (xcd_mode == 1 && k == 0)) ? 1u : 0u;
-                W.fetch8 = x8 + 16 * k;
-                W.n_in8 = x8 + 16 * k + 8;
-                W.n_out8 = xcd_mode == 2 ? x8 + 16 * (k + 1) + 8 : nullptr;
+                W.ctr = kCtr;
+                W.fetch8 = x8 + kCtr * (16 * k);
+                W.n_in8 = x8 + kCtr * (16 * k + 8);
+                W.n_out8 = xcd_mode == 2 ? x8 + kCtr * (16 * (k + 1) + 8) : nullptr;
                 if (!split || mb > 0) {
                     HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
                     if (k == 0)
@@ -1690,7 +1698,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                     hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_hist, c->d_cursor,
                                        nbins);
                     hipLaunchKernelGGL(sort_scatter_kernel, dim3(shade_blocks), dim3(kBlock), 0, c->stream,
-                                       (const float4*)c->d_q0, c->d_q1, (const uint32_t*)(n + k + 1), c->d_cursor);
+                                       (const float4*)c->d_q0, c->d_q1, (const uint32_t*)(n + kCtr * (k + 1)), c->d_cursor);
                     HIP_TRY(hipGetLastError());
                 }
             }
@@ -1738,7 +1746,18 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
     if (wf_debug && wf) {   // live paths entering each bounce of the last pass
         std::vector<uint32_t> nk(mb + 2, 0);
-        HIP_TRY(hipMemcpy(nk.data(), c->d_wfc, 4ull * (mb + 2), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> raw(ctr_stride * (mb + 2));
+        HIP_TRY(hipMemcpy(raw.data(), c->d_wfc, 4ull * raw.size(), hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < mb + 2; ++k) nk[k] = raw[ctr_stride * k];
+        if (xcd_mode == 2) {   // region counts (entering bounce k): 8 per launch
+            std::vector<uint32_t> r8(ctr_stride * 16 * (mb + 2));
+            HIP_TRY(hipMemcpy(r8.data(), c->d_wfc + 2 * ctr_stride * (mb + 2), 4ull * r8.size(),
+                              hipMemcpyDeviceToHost));
+            for (uint32_t k = 1; k <= mb; ++k) {
+                nk[k] = 0;
+                for (uint32_t g = 0; g < 8; ++g) nk[k] += r8[ctr_stride * (16 * k + 8 + g)];
+            }
+        }
         fprintf(stderr, "{\"zrt_last_pass_items\": %llu, \"live\": [", (unsigned long long)T);
         for (uint32_t k = 1; k <= mb; ++k) fprintf(stderr, "%s%u", k > 1 ? ", " : "", nk[k]);
         fprintf(stderr, "]}\n");
