@@ -11,7 +11,7 @@ OBJ       := build/obj
 HIPFLAGS  := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
              -Wall -Wno-unused-function -Iinclude
 CXXFLAGS  := -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Iinclude -pthread
-HDRS      := include/zrt.h $(SRC)/zrt_math.h $(SRC)/zrt_internal.h $(SRC)/dda.h $(SRC)/geometry.h
+HDRS      := include/zrt.h $(SRC)/zrt_math.h $(SRC)/zrt_internal.h $(SRC)/dda.h $(SRC)/geometry.h $(SRC)/device_geometry.h
 HOST_SRCS := $(filter-out $(SRC)/cli.cpp,$(wildcard $(SRC)/*.cpp))
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(HOST_SRCS))
 LIB       := $(PKG)/libzrt.so

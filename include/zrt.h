@@ -175,9 +175,23 @@ typedef struct zrt_outputs {
 } zrt_outputs;
 
 int zrt_context_create(const zrt_scene* scene, int device, zrt_context** out);
+/* Geometry.build + bakeInto (stage2.zig:44-164, main.zig:117-118) and the
+ * stage-3 upload in one step: the grid is built on `device` straight into the
+ * context's HBM arrays (no host copy of the baked scene).  Renders exactly as
+ * zrt_geometry_build + zrt_geometry_scene + zrt_context_create; the opt-in
+ * ZRT_MB=1 mailbox variant needs the host-built context. */
+int zrt_context_create_built(const float* positions, const float* normals, const float* texcoords,
+                             const uint32_t* material, uint32_t num_triangles, const uint32_t resolution[3],
+                             uint32_t num_materials, const zrt_material* materials, const float* texels,
+                             uint64_t num_texel_floats, int device, zrt_context** out);
 int zrt_context_render(zrt_context* ctx, const zrt_camera* camera, const zrt_render_config* cfg,
                        const zrt_outputs* outputs, zrt_stats* stats);
 void zrt_context_destroy(zrt_context* ctx);
+/* The context's grid and {num_refs, empty cells, min refs of a non-empty cell
+ * (0xFFFFFFFF if none), max refs of a cell}: the grid statistics the
+ * reference logs after Geometry.build (main.zig:117-118), without a host copy
+ * of the cells. */
+int zrt_context_grid_info(zrt_context* ctx, zrt_grid* grid, uint32_t info[4]);
 
 /* Pixels owned by `rank` (row-major image indices) in the packed output
  * order: tiles t = rank, rank+num_ranks, ... (row-major tile order), each

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from zig_raytracing_contest_amd import pngio, scenes
+from zig_raytracing_contest_amd import native, pngio, scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ZRT = os.path.join(ROOT, "zig_raytracing_contest_amd", "bin", "zrt")
@@ -45,8 +45,9 @@ def test_cli_argument_and_config_errors(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"ZRT_DEVICE_BUILD": "1"}, {"ZRT_DEVICES": "0,0"}],
-                         ids=["host-build", "device-build", "two-ranks"])
+@pytest.mark.parametrize("env", [{}, {"ZRT_DEVICE_BUILD": "0"}, {"ZRT_DEVICE_BUILD": "1"},
+                                 {"ZRT_DEVICES": "0,0"}],
+                         ids=["built-into-context", "host-build", "device-build", "two-ranks"])
 def test_cli_render_matches_oracle(tmp_path, oracle_mod, env):
     soup = scenes.get_scene("cornell")
     scenes.write_gltf(soup, str(tmp_path / "c.gltf"))
@@ -63,3 +64,11 @@ def test_cli_render_matches_oracle(tmp_path, oracle_mod, env):
     ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, c.aspect, 64, 48)
     rgb, _, _ = oracle_mod.OracleScene(loaded).render(ocam, 3, 4, oracle_mod.RNG_PATH, 0, 16)
     assert np.array_equal(img.reshape(-1, 3), rgb)
+    # the grid log line (main.zig:117-118 path) on every build path agrees
+    # with the host build's cells (pinned to the oracle, test_build_parity.py)
+    g = native.Geometry(loaded.pos, loaded.nrm, loaded.uv, loaded.mat, tuple(CFG["grid_resolution"]))
+    k = g.cells()[:, 1] - g.cells()[:, 0]
+    ne = int((k > 0).sum())
+    assert (f"Empty cells: {k.size - ne}/{k.size} ({100.0 * (k.size - ne) / k.size:.2f}%) min triangles: "
+            f"{int(k[k > 0].min())} max triangles: {int(k.max())} mean_triangles: {g.num_refs // ne}") \
+        in r.stderr

@@ -6,7 +6,7 @@ import time
 import numpy as np
 import pytest
 
-from zig_raytracing_contest_amd import native, scenes
+from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
 
 pytestmark = pytest.mark.gpu
 
@@ -39,3 +39,46 @@ def test_device_build_rejects_bad_args():
         native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, (0, 128, 128), device=0)
     with pytest.raises(native.ZrtError):
         native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, (8, 8, 8), device=99)
+
+
+# zrt_context_create_built: the device build feeding the render context
+# directly renders exactly what the host-built context renders (image, linear
+# radiance and the traversal counters), timed kernels and counting build.
+@pytest.mark.parametrize("name,res", [("cornell", (128, 128, 128)), ("contest", (128, 128, 128)),
+                                      ("sponza", (200, 64, 97)), ("sphere", (1, 1, 1))])
+@pytest.mark.parametrize("stats", [False, True])
+def test_context_built_on_device_renders_identically(name, res, stats):
+    soup = scenes.get_scene(name)
+    cam = camera_for(soup, None, None if soup.camera(None).aspect else 96, 54)
+    h = RenderScene(soup, res)
+    d = RenderScene(soup, res, device_build=True)
+    try:
+        cells = h.geometry.cells()
+        k = cells[:, 1] - cells[:, 0]
+        want = (h.geometry.num_refs, int((k == 0).sum()),
+                int(k[k > 0].min()) if (k > 0).any() else 0xFFFFFFFF, int(k.max()))
+        assert h.context.grid_info() == want
+        assert d.context.grid_info() == want
+        ih, rh = h.render(cam, num_samples=2, max_bounce=4, stats=stats, linear=True)
+        idv, rd = d.render(cam, num_samples=2, max_bounce=4, stats=stats, linear=True)
+        assert np.array_equal(ih, idv)
+        assert np.array_equal(rh["linear"].view(np.uint32), rd["linear"].view(np.uint32))
+        if stats:
+            ks = [k for k in rh["stats"] if not k.endswith("_ms")]
+            assert {k: rh["stats"][k] for k in ks} == {k: rd["stats"][k] for k in ks}
+    finally:
+        h.close()
+        d.close()
+
+
+def test_context_built_rejects_bad_args():
+    soup = scenes.get_scene("sphere")
+    mats = native.Scene()
+    keep = []
+    native.attach_materials(mats, soup.tex_desc, soup.texels, keep)
+    with pytest.raises(native.ZrtError):
+        native.Context.built(soup.pos, soup.nrm, soup.uv, soup.mat, mats, (0, 8, 8), 0)
+    with pytest.raises(native.ZrtError):
+        native.Context.built(soup.pos, soup.nrm, soup.uv, soup.mat + 1000, mats, (8, 8, 8), 0)
+    with pytest.raises(native.ZrtError):
+        native.Context.built(soup.pos, soup.nrm, soup.uv, soup.mat, mats, (8, 8, 8), 99)

@@ -68,11 +68,21 @@ def camera_for(soup, name=None, width=None, height=None) -> native.Camera:
 class RenderScene:
     """Baked scene on one GPU; `render` mirrors stage3.Scene.render."""
 
-    def __init__(self, soup, resolution=(128, 128, 128), device: int = -1, num_threads: int = 0):
+    def __init__(self, soup, resolution=(128, 128, 128), device: int = -1, num_threads: int = 0,
+                 device_build: bool = False):
+        """device_build: stage 2 on the GPU straight into the context
+        (zrt_context_create_built); otherwise host threads + upload."""
         self.soup = soup
+        self._keep = []
+        if device_build:
+            self.geometry = None
+            mats = native.Scene()
+            native.attach_materials(mats, soup.tex_desc, soup.texels, self._keep)
+            self.context = native.Context.built(soup.pos, soup.nrm, soup.uv, soup.mat, mats,
+                                                resolution, device)
+            return
         self.geometry = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, resolution,
                                         num_threads)
-        self._keep = []
         native.attach_materials(self.geometry.scene, soup.tex_desc, soup.texels, self._keep)
         self.context = native.Context(self.geometry.scene, device)
 

@@ -188,6 +188,7 @@ int main(int argc, char** argv) {
     zrt_camera cam;
     zrt_gltf* gltf = nullptr;
     zrt_geometry* geo = nullptr;
+    zrt_context* built = nullptr;   // one device: built there directly
     int rc;
     {
         const auto t = Clock::now();
@@ -210,33 +211,49 @@ int main(int argc, char** argv) {
         const auto t = Clock::now();
         info("Grid resolution: { " + std::to_string(cfg.res[0]) + ", " + std::to_string(cfg.res[1]) + ", " +
              std::to_string(cfg.res[2]) + " }");
-        // host threads (default: the arrays go to the device once, in the
-        // upload), or ZRT_DEVICE_BUILD=1: on the first render GPU
-        // (grid_build.hip), which round-trips them through the host (r01:
-        // 45 vs 30 ms for the contest stand-in).  Same arrays bit for bit.
+        // One device (default): the grid is built on it straight into the
+        // render context (zrt_context_create_built, r01: 5-9 ms against
+        // 36-97 ms for host build + upload).  Several devices, or
+        // ZRT_DEVICE_BUILD=0: host threads, then one upload per device;
+        // ZRT_DEVICE_BUILD=1: device build with the host round trip.  Same
+        // arrays, bit for bit, on every path.
         const char* db = getenv("ZRT_DEVICE_BUILD");
-        if (db && atoi(db) != 0) {
+        const int mode = db ? atoi(db) : (devices.size() == 1 ? 2 : 0);
+        uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0, ncells = 0, nrefs = 0;
+        if (mode == 2 && devices.size() == 1) {
             if (hip_warm.joinable()) hip_warm.join();
-            rc = zrt_geometry_build_device(pos, nrm, uv, mat, ntri, cfg.res, devices[0], &geo);
+            rc = zrt_context_create_built(pos, nrm, uv, mat, ntri, cfg.res, scene.num_materials, scene.materials,
+                                          scene.texels, scene.num_texel_floats, devices[0], &built);
+            if (rc != ZRT_OK) return fail("Geometry.build", rc);
+            uint32_t gi[4];
+            if ((rc = zrt_context_grid_info(built, nullptr, gi)) != ZRT_OK) return fail("Geometry.build", rc);
+            ncells = cfg.res[0] * cfg.res[1] * cfg.res[2];
+            nrefs = gi[0]; empty = gi[1]; mn = gi[2]; mx = gi[3];
         } else {
-            rc = zrt_geometry_build(pos, nrm, uv, mat, ntri, cfg.res, num_threads, &geo);
-        }
-        if (rc != ZRT_OK) return fail("Geometry.build", rc);
-        zrt_geometry_scene(geo, &scene);
-        uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0;
-        for (uint32_t c = 0; c < scene.num_cells; ++c) {
-            const uint32_t k = scene.cells[2 * c + 1] - scene.cells[2 * c];
-            if (!k) ++empty;
-            else { mn = std::min(mn, k); mx = std::max(mx, k); }
+            if (mode == 1) {
+                if (hip_warm.joinable()) hip_warm.join();
+                rc = zrt_geometry_build_device(pos, nrm, uv, mat, ntri, cfg.res, devices[0], &geo);
+            } else {
+                rc = zrt_geometry_build(pos, nrm, uv, mat, ntri, cfg.res, num_threads, &geo);
+            }
+            if (rc != ZRT_OK) return fail("Geometry.build", rc);
+            zrt_geometry_scene(geo, &scene);
+            ncells = scene.num_cells;
+            nrefs = scene.num_triangles;
+            for (uint32_t c = 0; c < scene.num_cells; ++c) {
+                const uint32_t k = scene.cells[2 * c + 1] - scene.cells[2 * c];
+                if (!k) ++empty;
+                else { mn = std::min(mn, k); mx = std::max(mx, k); }
+            }
         }
         char buf[256];
-        const uint32_t nonempty = scene.num_cells - empty;
+        const uint32_t nonempty = ncells - empty;
         snprintf(buf, sizeof buf, "Empty cells: %u/%u (%.2f%%) min triangles: %u max triangles: %u mean_triangles: %u",
-                 empty, scene.num_cells, 100.0 * empty / scene.num_cells, nonempty ? mn : 0xFFFFFFFFu, mx,
-                 nonempty ? scene.num_triangles / nonempty : 0);
+                 empty, ncells, 100.0 * empty / ncells, nonempty ? mn : 0xFFFFFFFFu, mx,
+                 nonempty ? nrefs / nonempty : 0);
         info(buf);
-        snprintf(buf, sizeof buf, "Unique triangle count: %u/%u (%.2f%%)", ntri, scene.num_triangles,
-                 scene.num_triangles ? 100.0 * ntri / scene.num_triangles : 0.0);
+        snprintf(buf, sizeof buf, "Unique triangle count: %u/%u (%.2f%%)", ntri, nrefs,
+                 nrefs ? 100.0 * ntri / nrefs : 0.0);
         info(buf);
         info("Compiled in " + fmt_duration(since(t)));
     }
@@ -247,7 +264,10 @@ int main(int argc, char** argv) {
         std::vector<int> rcs(devices.size(), ZRT_OK);
         std::vector<std::thread> th;
         for (size_t i = 0; i < devices.size(); ++i)
-            th.emplace_back([&, i] { rcs[i] = zrt_context_create(&scene, devices[i], &ctx[i]); });
+            th.emplace_back([&, i] {
+                if (built) ctx[i] = built;   // already on the device (one device)
+                else rcs[i] = zrt_context_create(&scene, devices[i], &ctx[i]);
+            });
         for (auto& x : th) x.join();
         for (int r : rcs)
             if (r != ZRT_OK) return fail("zrt_context_create", r);

@@ -39,6 +39,7 @@
 #include <new>
 #include <vector>
 
+#include "device_geometry.h"
 #include "geometry.h"
 
 using namespace zrt;
@@ -151,6 +152,30 @@ __global__ __launch_bounds__(kB) void bake_kernel(const float* __restrict__ pos,
     omat[i] = mat[t];
 }
 
+// bakeInto straight into the render context's layout (render.hip
+// context_init): Pos as 3 float4 (v0 | shape id 0, e1 | 0, e2 | 0), Data as 4
+// float4 (9 normal + 6 texcoord floats, material index bits).
+__global__ __launch_bounds__(kB) void ctx_bake_kernel(const float* __restrict__ pos, const float* __restrict__ nrm,
+                                                      const float* __restrict__ uv,
+                                                      const uint32_t* __restrict__ mat,
+                                                      const uint32_t* __restrict__ idx, uint32_t refs,
+                                                      float4* __restrict__ opos, float4* __restrict__ odata) {
+    const uint32_t i = blockIdx.x * kB + threadIdx.x;
+    if (i >= refs) return;
+    const uint32_t t = idx[i];
+    const float* p = pos + 9ull * t;
+    const v3 v0 = ld3(p), e1 = sub(ld3(p + 3), v0), e2 = sub(ld3(p + 6), v0);
+    opos[3ull * i] = make_float4(v0.x, v0.y, v0.z, 0.0f);
+    opos[3ull * i + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+    opos[3ull * i + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+    const float* nn = nrm + 9ull * t;
+    const float* uu = uv + 6ull * t;
+    odata[4ull * i] = make_float4(nn[0], nn[1], nn[2], nn[3]);
+    odata[4ull * i + 1] = make_float4(nn[4], nn[5], nn[6], nn[7]);
+    odata[4ull * i + 2] = make_float4(nn[8], uu[0], uu[1], uu[2]);
+    odata[4ull * i + 3] = make_float4(uu[3], uu[4], uu[5], __uint_as_float(mat[t]));
+}
+
 // Device buffers of one build, freed on every exit path.
 struct DevBufs {
     std::vector<void*> p;
@@ -175,11 +200,18 @@ struct DevBufs {
 
 uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kB - 1) / kB); }
 
+}  // namespace
+
+namespace {
+
+// geo: host result (zrt_geometry_build_device); dg: the render context's
+// device arrays instead (no host round trip).  Exactly one is non-null.
 int build_on_device(const float* positions, const float* normals, const float* texcoords,
-                    const uint32_t* material, uint32_t n, hipStream_t st, zrt_geometry* geo) {
+                    const uint32_t* material, uint32_t n, hipStream_t st, zrt_geometry* geo,
+                    const Grid& grid, uint32_t ncells_in, DeviceGeometry* dg) {
     DevBufs B;
-    const Grid g = geo->grid;
-    const uint32_t ncells = geo->ncells;
+    const Grid g = grid;
+    const uint32_t ncells = ncells_in;
     float* d_pos;
     uint32_t* d_range;
     unsigned long long *d_cnt, *d_off, *d_nrefs;
@@ -255,7 +287,12 @@ int build_on_device(const float* positions, const float* normals, const float* t
         GB_TRY(hipGetLastError());
     }
     uint2* d_cells;
-    GB_TRY(B.alloc(&d_cells, ncells));
+    if (dg) {
+        GB_TRY(hipMalloc((void**)&dg->cells, 8ull * std::max<uint32_t>(ncells, 1)));
+        d_cells = dg->cells;
+    } else {
+        GB_TRY(B.alloc(&d_cells, ncells));
+    }
     hipLaunchKernelGGL(cells_kernel, dim3(blocks_for(ncells)), dim3(kB), 0, st, d_first, d_count, ncells, d_cells);
     GB_TRY(hipGetLastError());
 
@@ -265,6 +302,21 @@ int build_on_device(const float* positions, const float* normals, const float* t
     GB_TRY(B.alloc(&d_nrm, 9ull * n));
     GB_TRY(B.alloc(&d_uv, 6ull * n));
     GB_TRY(B.alloc(&d_mat, n));
+    if (dg) {   // straight into the context's layout
+        dg->refs = refs;
+        GB_TRY(hipMalloc((void**)&dg->pos, 48ull * std::max<uint32_t>(refs, 1)));
+        GB_TRY(hipMalloc((void**)&dg->data, 64ull * std::max<uint32_t>(refs, 1)));
+        GB_TRY(hipMemcpyAsync(d_nrm, normals, 36ull * n, hipMemcpyHostToDevice, st));
+        GB_TRY(hipMemcpyAsync(d_uv, texcoords, 24ull * n, hipMemcpyHostToDevice, st));
+        GB_TRY(hipMemcpyAsync(d_mat, material, 4ull * n, hipMemcpyHostToDevice, st));
+        if (refs) {
+            hipLaunchKernelGGL(ctx_bake_kernel, dim3(blocks_for(refs)), dim3(kB), 0, st, d_pos, d_nrm, d_uv, d_mat,
+                               d_idx, refs, dg->pos, dg->data);
+            GB_TRY(hipGetLastError());
+        }
+        GB_TRY(hipStreamSynchronize(st));
+        return ZRT_OK;
+    }
     GB_TRY(B.alloc(&d_opos, 9ull * refs));
     GB_TRY(B.alloc(&d_odata, 15ull * refs));
     GB_TRY(B.alloc(&d_omat, refs));
@@ -326,7 +378,8 @@ extern "C" int zrt_geometry_build_device(const float* positions, const float* no
         try {
             geo->grid = scene_grid(positions, n, resolution);   // stage2.zig:44-57, host
             geo->ncells = resolution[0] * resolution[1] * resolution[2];
-            rc = build_on_device(positions, normals, texcoords, material, n, st, geo);
+            rc = build_on_device(positions, normals, texcoords, material, n, st, geo, geo->grid, geo->ncells,
+                                 nullptr);
         } catch (const std::bad_alloc&) {
             rc = ZRT_ERR_OUT_OF_MEMORY;
         }
@@ -340,4 +393,29 @@ extern "C" int zrt_geometry_build_device(const float* positions, const float* no
     }
     *out = geo;
     return ZRT_OK;
+}
+
+// Device build into a render context's arrays on the current device and
+// stream (render.hip zrt_context_create_built).  On failure the arrays
+// allocated so far are freed.
+int grid_build_into_device(const float* positions, const float* normals, const float* texcoords,
+                           const uint32_t* material, uint32_t n, const uint32_t resolution[3], hipStream_t st,
+                           Grid* grid, DeviceGeometry* dg) {
+    const int arc = check_build_args(positions, normals, texcoords, material, n, resolution);
+    if (arc != ZRT_OK) return arc;
+    *grid = scene_grid(positions, n, resolution);   // stage2.zig:44-57, host
+    int rc;
+    try {
+        rc = build_on_device(positions, normals, texcoords, material, n, st, nullptr, *grid,
+                             resolution[0] * resolution[1] * resolution[2], dg);
+    } catch (const std::bad_alloc&) {
+        rc = ZRT_ERR_OUT_OF_MEMORY;
+    }
+    if (rc != ZRT_OK) {
+        (void)hipStreamSynchronize(st);
+        for (void* q : {(void*)dg->cells, (void*)dg->pos, (void*)dg->data})
+            if (q) (void)hipFree(q);
+        *dg = DeviceGeometry();
+    }
+    return rc;
 }

@@ -35,6 +35,7 @@
 
 #include "zrt_internal.h"
 #include "dda.h"
+#include "device_geometry.h"
 
 using namespace zrt;
 
@@ -1216,19 +1217,26 @@ struct zrt_context {
     bool pix_valid = false;
 };
 
+static int validate_materials(const zrt_scene* s);
+
 static int validate_scene(const zrt_scene* s) {
     if (!s) return ZRT_ERR_INVALID_ARG;
     const uint64_t nc = (uint64_t)s->grid.resolution[0] * s->grid.resolution[1] * s->grid.resolution[2];
     if (nc == 0 || nc != s->num_cells || nc > 0x7FFFFFFFull || !s->cells) return ZRT_ERR_INVALID_ARG;
     if (s->num_triangles && (!s->triangles_pos || !s->triangles_data || !s->triangles_material))
         return ZRT_ERR_INVALID_ARG;
-    if (s->num_materials == 0 || !s->materials || !s->texels) return ZRT_ERR_INVALID_ARG;
     for (uint64_t c = 0; c < nc; ++c) {
         const uint32_t b = s->cells[2 * c], e = s->cells[2 * c + 1];
         if (b > e || e > s->num_triangles) return ZRT_ERR_INVALID_ARG;
     }
     for (uint32_t i = 0; i < s->num_triangles; ++i)
         if (s->triangles_material[i] >= s->num_materials) return ZRT_ERR_INVALID_ARG;
+    return validate_materials(s);
+}
+
+// Materials and texels only (textures inside the texel array).
+static int validate_materials(const zrt_scene* s) {
+    if (s->num_materials == 0 || !s->materials || !s->texels) return ZRT_ERR_INVALID_ARG;
     for (uint32_t m = 0; m < s->num_materials; ++m) {
         const zrt_texture* t[3] = {&s->materials[m].base_color, &s->materials[m].emissive,
                                    &s->materials[m].transparency};
@@ -1306,13 +1314,35 @@ static std::vector<uint32_t> shape_ids(const float* pos, uint32_t n) {
     return out;
 }
 
-static int context_init(zrt_context* c, const zrt_scene* s) {
+// Brick occupancy of the cells on the device (device-built contexts).
+__global__ __launch_bounds__(kBlock) void occ_bits_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                          uint32_t ncells, uint32_t sh, uint32_t nb0, uint32_t nb1,
+                                                          uint32_t* __restrict__ bits) {
+    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint2 c = cells[ci];
+        if (!(c.x < c.y)) continue;
+        const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / (r0 * r1);
+        const uint32_t b = ((z >> sh) * nb1 + (y >> sh)) * nb0 + (x >> sh);
+        atomicOr(&bits[b >> 5], 1u << (b & 31u));
+    }
+}
+
+static int context_base(zrt_context* c) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&c->ev_begin));
     HIP_TRY(hipEventCreate(&c->ev_end));
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, c->device));
     c->num_cus = prop.multiProcessorCount;
+    return ZRT_OK;
+}
+
+static int context_materials(zrt_context* c, const zrt_scene* s);
+static int context_occupancy(zrt_context* c, const uint32_t* host_cells);
+
+static int context_init(zrt_context* c, const zrt_scene* s) {
+    int rc = context_base(c);
+    if (rc != ZRT_OK) return rc;
     c->grid = s->grid;
     c->ncells = s->num_cells;
     c->nrefs = s->num_triangles;
@@ -1342,6 +1372,13 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
     HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
+    if ((rc = context_materials(c, s)) != ZRT_OK) return rc;
+    return context_occupancy(c, s->cells);
+}
+
+// Materials, texels, ziggurat tables (stage3.zig:125-129, Zig std ziggurat).
+static int context_materials(zrt_context* c, const zrt_scene* s) {
+    c->nmat = s->num_materials;
     std::vector<DevMat> mats(c->nmat);
     for (uint32_t m = 0; m < c->nmat; ++m) {
         const zrt_texture* t[3] = {&s->materials[m].base_color, &s->materials[m].emissive,
@@ -1363,6 +1400,12 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     zig_tables(zig, zig + 257);
     HIP_TRY(hipMalloc((void**)&c->d_zig, sizeof zig));
     HIP_TRY(hipMemcpy(c->d_zig, zig, sizeof zig, hipMemcpyHostToDevice));
+    return ZRT_OK;
+}
+
+// Brick occupancy from the host cells, or (host_cells null) from c->d_cells
+// on the device; then the work counters.
+static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     // brick occupancy bitmap: smallest power-of-two brick whose bitmap fits
     // the LDS budget (ZRT_OCC_BYTES, default 32 KiB; ZRT_OCC_SHIFT forces it)
     {
@@ -1370,7 +1413,7 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
         if (const char* e = getenv("ZRT_OCC_BYTES")) budget = (size_t)atoll(e);
         int forced = -1;
         if (const char* e = getenv("ZRT_OCC_SHIFT")) forced = atoi(e);
-        const uint32_t* r = s->grid.resolution;
+        const uint32_t* r = c->grid.resolution;
         uint32_t sh = 0;
         for (;; ++sh) {
             const uint64_t nb = (uint64_t)((r[0] + (1u << sh) - 1) >> sh) * ((r[1] + (1u << sh) - 1) >> sh) *
@@ -1385,17 +1428,27 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
         const uint64_t nb = (uint64_t)c->occ_nb[0] * c->occ_nb[1] * c->occ_nb[2];
         c->occ_words = (uint32_t)((nb + 31) / 32);
         std::vector<uint32_t> bits(std::max<uint32_t>(c->occ_words, 1), 0u);
-        for (uint32_t z = 0; z < r[2]; ++z)
-            for (uint32_t y = 0; y < r[1]; ++y)
-                for (uint32_t x = 0; x < r[0]; ++x) {
-                    const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
-                    if (s->cells[2 * ci] < s->cells[2 * ci + 1]) {
-                        const uint64_t b = ((uint64_t)(z >> sh) * c->occ_nb[1] + (y >> sh)) * c->occ_nb[0] + (x >> sh);
-                        bits[b >> 5] |= 1u << (b & 31);
-                    }
-                }
         HIP_TRY(hipMalloc((void**)&c->d_occ, bits.size() * 4));
-        HIP_TRY(hipMemcpy(c->d_occ, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+        if (host_cells) {
+            for (uint32_t z = 0; z < r[2]; ++z)
+                for (uint32_t y = 0; y < r[1]; ++y)
+                    for (uint32_t x = 0; x < r[0]; ++x) {
+                        const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
+                        if (host_cells[2 * ci] < host_cells[2 * ci + 1]) {
+                            const uint64_t b =
+                                ((uint64_t)(z >> sh) * c->occ_nb[1] + (y >> sh)) * c->occ_nb[0] + (x >> sh);
+                            bits[b >> 5] |= 1u << (b & 31);
+                        }
+                    }
+            HIP_TRY(hipMemcpy(c->d_occ, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+        } else {
+            HIP_TRY(hipMemsetAsync(c->d_occ, 0, bits.size() * 4, c->stream));
+            hipLaunchKernelGGL(occ_bits_kernel, dim3(std::min<uint32_t>((c->ncells + kBlock - 1) / kBlock, 8192)),
+                               dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells, sh, c->occ_nb[0],
+                               c->occ_nb[1], c->d_occ);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
     }
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
@@ -1420,6 +1473,104 @@ extern "C" int zrt_context_create(const zrt_scene* s, int device, zrt_context** 
     rc = context_init(c, s);
     if (rc != ZRT_OK) { zrt_context_destroy(c); return rc; }
     *out = c;
+    return ZRT_OK;
+}
+
+// Device-built context: Geometry.build + bakeInto (stage2.zig:44-164) on the
+// GPU straight into the context's arrays (grid_build.hip), no host copy of the
+// baked scene.  Same render results as zrt_geometry_build + zrt_context_create.
+extern "C" int zrt_context_create_built(const float* positions, const float* normals, const float* texcoords,
+                                        const uint32_t* material, uint32_t num_triangles,
+                                        const uint32_t resolution[3], uint32_t num_materials,
+                                        const zrt_material* materials, const float* texels,
+                                        uint64_t num_texel_floats, int device, zrt_context** out) {
+    if (!out) return ZRT_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!material) return ZRT_ERR_INVALID_ARG;
+    zrt_scene ms{};
+    ms.num_materials = num_materials;
+    ms.materials = materials;
+    ms.texels = texels;
+    ms.num_texel_floats = num_texel_floats;
+    int rc = validate_materials(&ms);
+    if (rc != ZRT_OK) return rc;
+    for (uint32_t i = 0; i < num_triangles; ++i)
+        if (material[i] >= num_materials) return ZRT_ERR_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) return ZRT_ERR_NO_DEVICE;
+    }
+    if (device >= n) return ZRT_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    zrt_context* c = new (std::nothrow) zrt_context();
+    if (!c) return ZRT_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    rc = context_base(c);
+    if (rc == ZRT_OK) {
+        zrt::Grid grid;
+        DeviceGeometry dg;
+        rc = grid_build_into_device(positions, normals, texcoords, material, num_triangles, resolution, c->stream,
+                                    &grid, &dg);
+        if (rc == ZRT_OK) {
+            for (int i = 0; i < 3; ++i) {
+                c->grid.bbox_min[i] = (&grid.bbox.min.x)[i];
+                c->grid.bbox_max[i] = (&grid.bbox.max.x)[i];
+                c->grid.resolution[i] = grid.res[i];
+                c->grid.cell_size[i] = (&grid.cell_size.x)[i];
+            }
+            c->ncells = resolution[0] * resolution[1] * resolution[2];
+            c->nrefs = dg.refs;
+            c->d_cells = dg.cells;
+            c->d_pos = dg.pos;
+            c->d_data = dg.data;
+            c->has_ids = false;   // ZRT_MB shape ids need the host build
+            if ((rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
+        }
+    }
+    if (rc != ZRT_OK) { zrt_context_destroy(c); return rc; }
+    *out = c;
+    return ZRT_OK;
+}
+
+// Empty cells and min/max refs of the non-empty ones (the CLI's grid log,
+// main.zig:117-118 + stage2 logging), reduced on the device.
+__global__ __launch_bounds__(kBlock) void grid_info_kernel(const uint2* __restrict__ cells, uint32_t ncells,
+                                                           uint32_t* __restrict__ out) {
+    uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0;
+    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint2 c = cells[ci];
+        const uint32_t k = c.y - c.x;
+        if (!k) ++empty;
+        else { mn = min(mn, k); mx = max(mx, k); }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        empty += __shfl_xor(empty, o);
+        mn = min(mn, (uint32_t)__shfl_xor(mn, o));
+        mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], empty);
+        atomicMin(&out[1], mn);
+        atomicMax(&out[2], mx);
+    }
+}
+
+extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t info[4]) {
+    if (!c || !info) return ZRT_ERR_INVALID_ARG;
+    DeviceGuard g(c->device);
+    if (grid) *grid = c->grid;
+    uint32_t h[3] = {0u, 0xFFFFFFFFu, 0u};
+    HIP_TRY(hipMemcpyAsync(c->d_counter, h, sizeof h, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(grid_info_kernel, dim3(std::min<uint32_t>((c->ncells + kBlock - 1) / kBlock, 2048)),
+                       dim3(kBlock), 0, c->stream, c->d_cells, c->ncells, c->d_counter);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h, c->d_counter, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    info[0] = c->nrefs;
+    info[1] = h[0];
+    info[2] = h[1];
+    info[3] = h[2];
     return ZRT_OK;
 }
 

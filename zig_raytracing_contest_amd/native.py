@@ -89,7 +89,7 @@ EXPORTS = [
     "zrt_error_string", "zrt_abi_version", "zrt_device_count", "zrt_device_warmup", "zrt_geometry_build",
     "zrt_geometry_build_device",
     "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
-    "zrt_context_create", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
+    "zrt_context_create", "zrt_context_create_built", "zrt_context_grid_info", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
     "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
     "zrt_camera_from_matrix", "zrt_probe",
 ]
@@ -118,6 +118,11 @@ def lib():
     L.zrt_render.argtypes = [C.POINTER(Scene), C.POINTER(Camera), C.POINTER(RenderConfig),
                              C.c_void_p, C.POINTER(Stats)]
     L.zrt_context_create.argtypes = [C.POINTER(Scene), C.c_int, C.POINTER(C.c_void_p)]
+    L.zrt_context_create_built.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                           C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(Material),
+                                           C.POINTER(C.c_float), C.c_uint64, C.c_int,
+                                           C.POINTER(C.c_void_p)]
+    L.zrt_context_grid_info.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
     L.zrt_context_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig),
                                      C.POINTER(Outputs), C.POINTER(Stats)]
     L.zrt_context_destroy.argtypes = [C.c_void_p]
@@ -248,6 +253,28 @@ class Context:
         h = C.c_void_p()
         check(lib().zrt_context_create(C.byref(scene), device, C.byref(h)), "zrt_context_create")
         self._h = h
+
+    @classmethod
+    def built(cls, pos, nrm, uv, mat, materials: Scene, resolution=(128, 128, 128), device: int = -1):
+        """zrt_context_create_built: grid built on the GPU straight into the
+        context (materials/texels taken from `materials`' material fields)."""
+        keep = [np.ascontiguousarray(pos, np.float32), np.ascontiguousarray(nrm, np.float32),
+                np.ascontiguousarray(uv, np.float32), np.ascontiguousarray(mat, np.uint32)]
+        res = (C.c_uint32 * 3)(*resolution)
+        h = C.c_void_p()
+        check(lib().zrt_context_create_built(*[k.ctypes.data for k in keep], keep[3].size, res,
+                                             materials.num_materials, materials.materials,
+                                             materials.texels, materials.num_texel_floats, device,
+                                             C.byref(h)), "zrt_context_create_built")
+        self = cls.__new__(cls)
+        self._h = h
+        return self
+
+    def grid_info(self):
+        """(num_refs, empty cells, min refs of a non-empty cell, max refs)."""
+        info = (C.c_uint32 * 4)()
+        check(lib().zrt_context_grid_info(self._h, None, info), "zrt_context_grid_info")
+        return tuple(int(x) for x in info)
 
     def close(self):
         if getattr(self, "_h", None) is not None and _lib is not None:
