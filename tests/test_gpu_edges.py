@@ -1,0 +1,117 @@
+"""GPU edge cases against the CPU oracle, bit for bit (image, linear radiance
+and the traversal counters), on both ways of making a context (host build +
+upload, and the device build straight into the context):
+
+- image sizes that are not multiples of the 8x8 wave block or the 64x64 tile
+  (1x1, 7x13, 65x3, 129x67): the ragged edges of stage3.zig:228-229's split;
+- a camera inside the grid's bbox (Grid.traceRay's origin-inside branch,
+  linalg.zig:443-469) and one that sees only sky (getEnvColor, stage3.zig:144-150);
+- degenerate triangles (zero area, collinear, repeated vertices) mixed into a
+  mesh: Moller-Trumbore's det == 0 path (linalg.zig:683-722) and the SAT
+  build (linalg.zig:516-563);
+- a one-triangle scene, grid resolutions 1x1x1 and non-cubic;
+- max_bounce 0 (primary rays only).
+"""
+import dataclasses
+import math
+
+import numpy as np
+import pytest
+
+from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_camera(soup, eye, target, yfov_deg=50.0):
+    cam = scenes.CameraDef("Edge", scenes.look_at(eye, target), math.radians(yfov_deg), None)
+    return dataclasses.replace(soup, cameras=[cam])
+
+
+def _degenerate_sphere():
+    s = scenes.get_scene("sphere")
+    v = np.array([[0.2, 0.1, 0.9], [0.2, 0.1, 0.9], [0.2, 0.1, 0.9],      # one point
+                  [-0.5, 0.0, 1.1], [0.0, 0.0, 1.1], [0.5, 0.0, 1.1],    # collinear
+                  [0.3, -0.4, 1.05], [0.3, -0.4, 1.05], [0.6, 0.2, 1.05],  # two equal vertices
+                  [-0.2, 0.3, 1.2], [0.1, 0.3, 1.2], [-0.2, 0.6, 1.2]],  # a proper one on top
+                 np.float32).reshape(4, 9)
+    n = np.tile(np.array([0, 0, 1], np.float32), (4, 3))
+    uv = np.zeros((4, 6), np.float32)
+    return dataclasses.replace(s, name="sphere_degenerate", pos=np.concatenate([s.pos, v]),
+                               nrm=np.concatenate([s.nrm, n]), uv=np.concatenate([s.uv, uv]),
+                               mat=np.concatenate([s.mat, np.zeros(4, s.mat.dtype)]))
+
+
+def _one_triangle():
+    s = scenes.get_scene("sphere")
+    pos = np.array([[-1, -1, 0, 1, -1, 0, 0, 1, 0]], np.float32)
+    nrm = np.tile(np.array([0, 0, 1], np.float32), (1, 3))
+    return dataclasses.replace(s, name="one_triangle", pos=pos, nrm=nrm,
+                               uv=np.zeros((1, 6), np.float32), mat=np.zeros(1, s.mat.dtype))
+
+
+def _cornell_inside():
+    s = scenes.get_scene("cornell")
+    lo = s.pos.reshape(-1, 3).min(0)
+    hi = s.pos.reshape(-1, 3).max(0)
+    mid = (lo + hi) / 2
+    eye = mid + (hi - lo) * np.array([0.1, 0.15, 0.2])
+    return _with_camera(s, tuple(float(x) for x in eye), tuple(float(x) for x in lo), 70.0)
+
+
+def _sky_only():
+    return _with_camera(scenes.get_scene("sphere"), (0, 0, 3), (0, 0, 6))
+
+
+SCENES = {"sphere": lambda: scenes.get_scene("sphere"), "degenerate": _degenerate_sphere,
+          "one_triangle": _one_triangle, "cornell_inside": _cornell_inside, "sky_only": _sky_only}
+
+# (scene, w, h, spp, max_bounce, grid resolution)
+CASES = [("sphere", 1, 1, 3, 4, (128, 128, 128)),
+         ("sphere", 7, 13, 2, 4, (128, 128, 128)),
+         ("sphere", 65, 3, 2, 4, (128, 128, 128)),
+         ("sphere", 129, 67, 1, 4, (128, 128, 128)),
+         ("degenerate", 48, 40, 2, 4, (128, 128, 128)),
+         ("degenerate", 48, 40, 2, 4, (3, 5, 2)),
+         ("one_triangle", 40, 40, 2, 4, (128, 128, 128)),
+         ("one_triangle", 40, 40, 2, 4, (1, 1, 1)),
+         ("cornell_inside", 64, 48, 2, 4, (128, 128, 128)),
+         ("cornell_inside", 64, 48, 2, 4, (31, 64, 17)),
+         ("cornell_inside", 64, 48, 4, 0, (128, 128, 128)),
+         ("sky_only", 32, 24, 2, 4, (128, 128, 128))]
+
+
+@pytest.fixture(scope="module")
+def soups():
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            cache[name] = SCENES[name]()
+        return cache[name]
+    return get
+
+
+@pytest.mark.parametrize("device_build", [False, True], ids=["host-build", "device-build"])
+@pytest.mark.parametrize("name,w,h,spp,mb,res", CASES)
+def test_edge_render_bitexact_vs_oracle(oracle_mod, soups, name, w, h, spp, mb, res, device_build):
+    soup = soups(name)
+    cam = camera_for(soup, None, w, h)
+    rs = RenderScene(soup, res, device_build=device_build)
+    try:
+        img, out = rs.render(cam, num_samples=spp, max_bounce=mb, stats=True, linear=True)
+        fast, _ = rs.render(cam, num_samples=spp, max_bounce=mb)   # timed kernels
+    finally:
+        rs.close()
+    c = soup.camera(None)
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
+    rgb, lin, ctr = oracle_mod.OracleScene(soup, res).render(ocam, spp, mb, oracle_mod.RNG_PATH, 0, 16)
+    pix = native.tile_pixels(cam.w, cam.h)
+    assert np.array_equal(out["linear"].view(np.uint32), lin[pix].view(np.uint32))
+    assert np.array_equal(img.reshape(-1, 3), rgb)
+    assert np.array_equal(fast, img)
+    st = out["stats"]
+    assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == \
+        tuple(int(x) for x in ctr[:4])
+    if name == "sky_only":   # the walk still runs: the box behind the camera is entered
+        assert st["hits"] == 0
