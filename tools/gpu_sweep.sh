@@ -1,10 +1,8 @@
 #!/bin/bash
-# parity tests (fast) then a variant sweep
+# one-process A/B sweep of env variants on cfg3 (args: kbench --var values)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
-case $rc in 0|1) ;; *) exit $rc;; esac
-timeout -k 10 600 python tools/kbench.py "$@" > gpurun_out/sweep.log 2>&1
-rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log | tail -20
-exit $rc
+args=()
+for v in "$@"; do args+=(--var "$v"); done
+timeout -k 10 500 python -u tools/kbench.py --spp 64 --reps 2 "${args[@]}" > gpurun_out/sweep.log 2>&1
+rc=$?; cat gpurun_out/sweep.log; exit $rc

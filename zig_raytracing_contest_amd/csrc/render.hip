@@ -1715,6 +1715,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         } else {
             ZRT_WF_SWITCH(wf_kernel)
         }
+        // the primary launch alone at another occupancy (tuning sweeps only)
+        if (const char* e0 = getenv("ZRT_WF_MINW0"); e0 && !split && !wave_mode && !mbe && tbv == kTriBatch) {
+            switch (atoi(e0)) {
+                case 4: wf_first = (WfFn)wf_kernel<kTriBatch, 4, true>; break;
+                case 5: wf_first = (WfFn)wf_kernel<kTriBatch, 5, true>; break;
+                case 6: wf_first = (WfFn)wf_kernel<kTriBatch, 6, true>; break;
+                case 8: wf_first = (WfFn)wf_kernel<kTriBatch, 8, true>; break;
+                default: break;
+            }
+        }
 #undef ZRT_WF_SWITCH
 #undef ZRT_WF_PICK
     }
