@@ -1124,9 +1124,15 @@ using TraceFn = void (*)(const TraceParams);
 // few spills land outside the DDA loop and 6 waves hide more memory latency
 // than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
 constexpr int kMinWaves = 6;
-// wf_kernel: 7 waves/SIMD (72 VGPRs): cfg3 64 spp 1826 vs 1786 and 1783 vs
-// 1775 Mrays/s against 6 in two r01 sweeps; 8 (64 VGPRs) spills: 1503.
-constexpr int kWfMinWaves = 7;
+// wf_kernel bounce launches: 6 waves/SIMD (80 VGPRs, 88 B/lane of spills
+// against 128 at 7).  Early r01 sweeps had 7 ahead by 1-2%, but 7 is at the
+// mercy of the spill allocator: the final r01 kernel at 7 ran cfg3 (256 spp)
+// at 1933 Mrays/s against 2108 at 6 on the same box, cfg5 678 vs 777, cfg2
+// 2005 vs 1968.  The primary launch (coherent rays, the larger share on
+// sparse scenes) keeps 7 (kWfMinWaves0): 2113-2114 on cfg3.  8 (64 VGPRs)
+// spills: 1503.
+constexpr int kWfMinWaves = 6;
+constexpr int kWfMinWaves0 = 7;
 constexpr int kSplitMinWaves = 6;
 
 template <int MAXB>
@@ -1715,12 +1721,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         } else {
             ZRT_WF_SWITCH(wf_kernel)
         }
-        // the primary launch alone at another occupancy (tuning sweeps only)
-        if (const char* e0 = getenv("ZRT_WF_MINW0"); e0 && !split && !wave_mode && !mbe && tbv == kTriBatch) {
+        // the primary launch alone at another occupancy (kWfMinWaves0 unless
+        // ZRT_WF_MINW sets both; ZRT_WF_MINW0 for tuning sweeps)
+        const char* e0 = getenv("ZRT_WF_MINW0");
+        if (!e0 && !e) e0 = kWfMinWaves0 == 7 ? "7" : "6";
+        if (e0 && !split && !wave_mode && !(mbe && atoi(mbe) == 1) && tbv == kTriBatch) {
             switch (atoi(e0)) {
                 case 4: wf_first = (WfFn)wf_kernel<kTriBatch, 4, true>; break;
                 case 5: wf_first = (WfFn)wf_kernel<kTriBatch, 5, true>; break;
                 case 6: wf_first = (WfFn)wf_kernel<kTriBatch, 6, true>; break;
+                case 7: wf_first = (WfFn)wf_kernel<kTriBatch, 7, true>; break;
                 case 8: wf_first = (WfFn)wf_kernel<kTriBatch, 8, true>; break;
                 default: break;
             }
