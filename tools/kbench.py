@@ -14,12 +14,14 @@ from zig_raytracing_contest_amd import camera_for, native, scenes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg3")
-ap.add_argument("--spp", type=int, default=64)
+ap.add_argument("--spp", type=int, default=64, help="0: the config's own spp")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--cell-stats", action="store_true", help="one counting render first (ZRT_CELL_STATS)")
 ap.add_argument("--var", action="append", default=[], help="ENV=VAL[,ENV=VAL] per variant")
 a = ap.parse_args()
 cfg = scenes.CONFIGS[a.config]
+if a.spp == 0:
+    a.spp = cfg["spp"]
 soup = scenes.get_scene(cfg["scene"])
 cam = camera_for(soup, cfg["camera"], cfg["width"], cfg["height"])
 geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
