@@ -17,7 +17,9 @@ HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.o,$(HOST_SRCS))
 LIB       := $(PKG)/libzrt.so
 CLI       := $(PKG)/bin/zrt
 
-all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) oracle
+PROBE     := tools/bin/dpp_probe
+
+all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) $(PROBE) oracle
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) $(wildcard $(SRC)/*.h)
 	@mkdir -p $(OBJ)
@@ -36,11 +38,16 @@ $(CLI): $(SRC)/cli.cpp $(LIB) include/zrt.h
 	@mkdir -p $(PKG)/bin
 	$(CXX) $(CXXFLAGS) -o $@ $(SRC)/cli.cpp -L$(PKG) -lzrt -Wl,-rpath,'$$ORIGIN/..' -Wl,-rpath,$(ROCM)/lib
 
+# DPP-under-partial-EXEC check (DESIGN.md §5, round 1's park-mode fault)
+$(PROBE): tools/dpp_probe.hip
+	@mkdir -p tools/bin
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB) $(PKG)/bin
+	rm -rf build $(LIB) $(PKG)/bin tools/bin
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean oracle

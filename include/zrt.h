@@ -104,7 +104,9 @@ typedef struct zrt_render_config {
     uint32_t num_ranks;              /* tiles t with t % num_ranks == rank */
     uint32_t tile_size;              /* square tile edge in pixels, 0 = 64 */
     uint32_t flags;                  /* ZRT_FLAG_* */
-    uint32_t _reserved[5];
+    uint32_t samples_per_pass;       /* samples of every pixel per device pass, 0 = as many as fit
+                                        40 GiB of path queues (the image is the same for any value) */
+    uint32_t _reserved[4];
 } zrt_render_config;
 
 #define ZRT_FLAG_COUNT_STATS  0x1u   /* count cells/tests/hits (slower kernel variant) */
@@ -178,8 +180,7 @@ int zrt_context_create(const zrt_scene* scene, int device, zrt_context** out);
 /* Geometry.build + bakeInto (stage2.zig:44-164, main.zig:117-118) and the
  * stage-3 upload in one step: the grid is built on `device` straight into the
  * context's HBM arrays (no host copy of the baked scene).  Renders exactly as
- * zrt_geometry_build + zrt_geometry_scene + zrt_context_create; the opt-in
- * ZRT_MB=1 mailbox variant needs the host-built context. */
+ * zrt_geometry_build + zrt_geometry_scene + zrt_context_create. */
 int zrt_context_create_built(const float* positions, const float* normals, const float* texcoords,
                              const uint32_t* material, uint32_t num_triangles, const uint32_t resolution[3],
                              uint32_t num_materials, const zrt_material* materials, const float* texels,
@@ -222,14 +223,19 @@ int zrt_camera_from_matrix(const float matrix[16], float yfov, int has_aspect_ra
 enum {
     ZRT_PROBE_TRIANGLE = 0,   /* in n*15 (v0,v1,v2,orig,dir) -> out n*4 (hit,t,u,v) */
     ZRT_PROBE_BBOX = 1,       /* in n*12 (min,max,orig,dir) -> out n*2 (hit,t) */
-    ZRT_PROBE_DDA = 2,        /* in n*12 (min,max,orig,dir) + res in aux -> out n*(1+4*64) */
+    ZRT_PROBE_DDA = 2,        /* in n*12 (min,max,orig,dir) + res u32[3] in aux -> out n*(4+4*64):
+                                 steps (-1 miss, -2 bad linear index), first cell, (cell, t) per next() */
     ZRT_PROBE_TO_RGB = 3,     /* in n*3 -> out n*3 (as float) */
     ZRT_PROBE_RNG_F32 = 4,    /* in n*3 u32 (seed_lo,pixel,sample) -> out n*16 floats */
     ZRT_PROBE_RNG_NORM = 5,   /* same -> out n*16 floats */
     ZRT_PROBE_EXP_LOG = 6,    /* in n doubles -> out n*2 doubles (exp, log) */
     ZRT_PROBE_TEXTURE = 7,    /* in n*2 (u,v) + aux texture -> out n*3 */
+    ZRT_PROBE_TRIANGLE_FLAT = 8, /* as TRIANGLE, through the branch-free test of the park kernel */
 };
 int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device);
+/* Comma-separated substrings of the mangled names of the timed kernel
+ * instantiations in the gfx950 code object (build checks; no HIP call). */
+const char* zrt_timed_kernels(void);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,129 @@
+"""The drop-in boundary on the GPU, exactly as its callers use it.
+
+* zrt_render -- the one-shot export INTEGRATION.md binds in place of
+  Scene.render (stage3.zig:247, called at main.zig:126): upload, render,
+  download, free -- against the committed golden renders (tests/golden/,
+  tools/make_golden.py), no oracle at run time.
+* bench.py's multi-GPU step (dist.render_gathered): render into a torch
+  device buffer through zrt_outputs.device_rgb_packed, then the gather of
+  packed RGB8 tiles to rank 0 -- over a real "nccl" (RCCL) process group at
+  world size 1, and over gloo with two ranks sharing the GPU; both must equal
+  the single-process host-copy image.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import torch  # noqa: F401  (first: libzrt then binds to torch's HIP runtime, as in bench.py)
+
+from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
+from zig_raytracing_contest_amd import dist as zdist
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name", ["sphere", "cornell", "contest"])
+def test_oneshot_zrt_render_matches_golden(name):
+    g = np.load(os.path.join(GOLD, f"render_{name}.npz"), allow_pickle=False)
+    soup = scenes.get_scene(name)
+    cname = str(g["camera"]) or None
+    c = soup.camera(cname)
+    cam = camera_for(soup, cname, None if c.aspect else int(g["w"]), int(g["h"]))
+    geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
+    keep = []
+    native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
+    img, st = native.render_oneshot(geo.scene, cam, int(g["spp"]), int(g["max_bounce"]), seed=int(g["seed"]))
+    assert np.array_equal(img.reshape(-1, 3), g["rgb"])
+    assert st["samples"] == cam.w * cam.h * int(g["spp"])
+    assert st["segments"] == int(g["counters"][0])
+
+
+def test_oneshot_zrt_render_rejects_bad_input():
+    soup = scenes.get_scene("sphere")
+    geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, resolution=(8, 8, 8))
+    keep = []
+    native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
+    cam = camera_for(soup, None, 16, 16)
+    with pytest.raises(native.ZrtError) as e:
+        native.render_oneshot(geo.scene, cam, 0, 4)
+    assert e.value.status == -1
+    with pytest.raises(native.ZrtError) as e:
+        native.render_oneshot(geo.scene, cam, 1, 4, device=99)
+    assert e.value.status == -2
+
+
+def test_bench_gather_path_nccl_world1():
+    import torch
+    import torch.distributed as dist
+    soup = scenes.get_scene("contest")
+    cam = camera_for(soup, "Camera 1", None, 90)
+    rs = RenderScene(soup, device=0)
+    ref, _ = rs.render(cam, num_samples=2, max_bounce=4)              # host copy
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        buf = torch.zeros(zdist.max_packed(cam.w, cam.h, 1) * 3, dtype=torch.uint8, device="cuda:0")
+        img, res = zdist.render_gathered(rs.context, cam, 2, 4, 0, 1, dist, buf)
+        torch.cuda.synchronize()
+        assert np.array_equal(img.cpu().numpy(), ref)
+        assert res["stats"]["samples"] == cam.w * cam.h * 2
+    finally:
+        dist.destroy_process_group()
+        rs.close()
+
+
+_RANK_SCRIPT = r"""
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["ZRT_ROOT"])
+from zig_raytracing_contest_amd import RenderScene, camera_for, scenes
+from zig_raytracing_contest_amd import dist as zdist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+soup = scenes.get_scene("contest")
+cam = camera_for(soup, "Camera 1", None, 180)
+rs = RenderScene(soup, device=0)
+res = rs.context.render(cam, 2, 4, rank=rank, num_ranks=world, packed=True)
+buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8)
+buf[: res["packed"].size] = torch.from_numpy(res["packed"].reshape(-1))
+img = zdist.gather_image(buf, cam.w, cam.h, rank, world, dist)
+if rank == 0:
+    np.save(os.environ["ZRT_OUT"], img.numpy())
+dist.barrier()
+dist.destroy_process_group()
+rs.close()
+"""
+
+
+def test_two_ranks_on_one_gpu_gather_gloo(tmp_path):
+    soup = scenes.get_scene("contest")
+    cam = camera_for(soup, "Camera 1", None, 180)
+    rs = RenderScene(soup, device=0)
+    ref, _ = rs.render(cam, num_samples=2, max_bounce=4)
+    rs.close()
+    port, out = _free_port(), str(tmp_path / "img.npy")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   ZRT_ROOT=ROOT, ZRT_OUT=out)
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK_SCRIPT], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    assert np.array_equal(np.load(out), ref)

@@ -3,9 +3,10 @@
 The timed wf_kernel instantiations must not touch scratch memory inside the
 cell walk: when the 7-wave bounce kernel did (2-3 spill reloads per trip), the
 bounce launches ran 9% slower with bit-identical output, which no parity test
-can see.  tools/spill_check.py does the disassembly; the
-8-wave instantiation (64 VGPRs against a ~100-VGPR working set) is the control
-that shows the check finds walk spills when they are there.
+can see.  tools/spill_check.py does the disassembly; which
+instantiations are timed comes from libzrt itself (zrt_timed_kernels), so a
+change of the launch constants cannot leave the check on a stale kernel.  A
+synthetic disassembly is the control that the loop scan finds walk spills.
 """
 import os
 import shutil
@@ -25,6 +26,8 @@ def code():
         pytest.skip("build/obj/render.o not built (make)")
     if not shutil.which(os.path.join(spill_check.LLVM, "llvm-objdump")):
         pytest.skip("ROCm llvm tools absent")
+    if not spill_check.has_gfx950(OBJ):
+        pytest.skip("render.o holds no gfx950 code object (ARCH= build)")
     return spill_check, spill_check.kernels(spill_check.disassemble(OBJ))
 
 
@@ -36,13 +39,29 @@ def _walk_scratch(sc, ks, sub):
     return max(s for _, _, s in loops)
 
 
-@pytest.mark.parametrize("sub", ["wf_kernelILi2ELi7ELb1ELb0EE", "wf_kernelILi2ELi6ELb0ELb0EE"])
-def test_timed_kernels_do_not_spill_in_the_walk(code, sub):
-    sc, ks = code
-    assert sub in sc.TIMED
-    assert _walk_scratch(sc, ks, sub) == 0
+def test_timed_kernel_names_come_from_the_library():
+    import spill_check
+    t = spill_check.timed()
+    assert len(t) == 2 and t[0].startswith("wf_kernel") and t[1].startswith("wf_kernel")
 
 
-def test_spill_check_sees_walk_spills(code):
+def test_timed_kernels_do_not_spill_in_the_walk(code):
     sc, ks = code
-    assert _walk_scratch(sc, ks, "wf_kernelILi2ELi8ELb0ELb0EE") > 0
+    for sub in sc.timed():
+        assert _walk_scratch(sc, ks, sub) == 0, sub
+
+
+def test_spill_check_sees_walk_spills():
+    import spill_check as sc
+    base = 0x1000
+    lines = [
+        (base + 0x00, "  s_mov_b32 s0, 0  // 000000001000:"),
+        (base + 0x04, "  global_load_dwordx4 v[0:3], v[4:5], off  // 000000001004:"),
+        (base + 0x0c, "  scratch_load_dword v7, off, s0 offset:16  // 00000000100C:"),
+        (base + 0x14, "  v_add_f32 v1, v1, v2  // 000000001014:"),
+        (base + 0x18, "  s_cbranch_vccnz 65532 <_Zkern+0x4>  // 000000001018:"),
+    ]
+    loops = sc.walk_spills(lines)
+    assert loops and max(s for _, _, s in loops) == 1
+    clean = [l for l in lines if "scratch" not in l[1]]
+    assert max(s for _, _, s in sc.walk_spills(clean)) == 0

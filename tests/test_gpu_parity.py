@@ -41,6 +41,11 @@ def test_probe_triangle(oracle_mod, rng):
     # edge cases: axis-aligned, back face, det just below/above 1e-8, degenerate
     inp = np.concatenate([v, o, d], 1).astype(np.float32)
     out = native.probe(native.PROBE_TRIANGLE, inp, n, (n, 4))
+    flat = native.probe(native.PROBE_TRIANGLE_FLAT, inp, n, (n, 4))
+    # the park kernel's branch-free test: same answer, same t/u/v on hits
+    assert np.array_equal(flat[:, 0], out[:, 0])
+    hm = out[:, 0] == 1
+    assert np.array_equal(flat[hm], out[hm])
     hits = 0
     for i in range(n):
         h, tuv = oracle_mod.tri_intersect(v[i, 0:3], v[i, 3:6], v[i, 6:9], o[i], d[i])
@@ -60,6 +65,8 @@ def test_probe_triangle_culling_edges(oracle_mod):
              ((0.25, 0.25, 1), (1, 0, 0))]                                     # parallel: det=0
     inp = np.array([list(tri) + list(o) + list(d) for o, d in cases], np.float32)
     out = native.probe(native.PROBE_TRIANGLE, inp, len(cases), (len(cases), 4))
+    flat = native.probe(native.PROBE_TRIANGLE_FLAT, inp, len(cases), (len(cases), 4))
+    assert np.array_equal(flat[:, 0], out[:, 0])
     for i, (o, d) in enumerate(cases):
         h, tuv = oracle_mod.tri_intersect(tri[0:3], tri[3:6], tri[6:9], o, d)
         assert bool(out[i, 0]) == h
@@ -68,41 +75,85 @@ def test_probe_triangle_culling_edges(oracle_mod):
     assert out[0, 0] == 1 and out[1, 0] == 0 and out[6, 0] == 0
 
 
+def _dda_probe(lo, hi, o, d, res):
+    inp = np.array([list(lo) + list(hi) + list(o) + list(d)], np.float32)
+    return native.probe(native.PROBE_DDA, inp, 1, (1, native.DDA_PROBE_WIDTH),
+                        aux=np.array(res, np.uint32))[0]
+
+
+# The reference's own DDA known-answer tests (linalg.zig:583-681, grid 5^3
+# over [0,5]^3) through the kernels' dda_init + DDA_STEP: exact cells, t
+# within the reference's 1e-4, and t bit-equal to the oracle.
+DDA_KATS = [((0.5, 0.5, 0.5), "n210", (0, 0, 0), [
+                ((1, 0, 0), 0.559017002), ((1, 1, 0), 1.11803400), ((2, 1, 0), 1.67705106),
+                ((3, 1, 0), 2.79508495), ((3, 2, 0), 3.35410213), ((4, 2, 0), 3.91311883)]),
+            ((0.5, 10.0, 0.5), (0, -1, 0), (0, 4, 0), [
+                ((0, 3, 0), 6), ((0, 2, 0), 7), ((0, 1, 0), 8), ((0, 0, 0), 9)]),
+            ((0.5, -5.0, 0.5), (0, 1, 0), (0, 0, 0), [
+                ((0, 1, 0), 6), ((0, 2, 0), 7), ((0, 3, 0), 8), ((0, 4, 0), 9)]),
+            ((0.5, 0.5, 0.5), "n110", (0, 0, 0), [
+                ((0, 1, 0), 0.707106769), ((1, 1, 0), 0.707106769), ((1, 2, 0), 2.12132024),
+                ((2, 2, 0), 2.12132024), ((2, 3, 0), 3.53553390), ((3, 3, 0), 3.53553390),
+                ((3, 4, 0), 4.94974756), ((4, 4, 0), 4.94974756)])]
+
+
+@pytest.mark.parametrize("k", range(len(DDA_KATS)))
+def test_probe_dda_reference_kats(oracle_mod, k):
+    orig, d, first, seq = DDA_KATS[k]
+    d = {"n210": _norm([2, 1, 0]), "n110": _norm([1, 1, 0])}.get(d, d) if isinstance(d, str) else d
+    out = _dda_probe((0, 0, 0), (5, 5, 5), orig, d, (5, 5, 5))
+    steps = int(out[0])
+    assert steps == len(seq) + 1                      # + the final next() = +inf
+    assert tuple(int(x) for x in out[1:4]) == first
+    got = out[4:4 + 4 * steps].reshape(steps, 4)
+    for i, (cell, t) in enumerate(seq):
+        assert tuple(int(x) for x in got[i, :3]) == cell, (i, got[i])
+        assert abs(float(got[i, 3]) - t) <= 1e-4, (i, got[i, 3], t)
+    assert got[-1, 3] == np.inf
+    tr = oracle_mod.grid_trace((0, 0, 0), (5, 5, 5), (5, 5, 5), orig, d, 64)
+    f, cells, ts = tr
+    assert tuple(int(x) for x in f) == first
+    assert np.array_equal(got[:, :3].astype(np.uint32), cells)
+    assert np.array_equal(got[:, 3].astype(np.float32), ts)
+
+
 def test_probe_bbox_and_dda(oracle_mod, rng):
-    # linalg.zig KAT cases + random rays on odd grids
-    cases = [((0, 0, 0), (5, 5, 5), (0.5, 0.5, 0.5), _norm([2, 1, 0])),
-             ((0, 0, 0), (5, 5, 5), (0.5, 10, 0.5), (0, -1, 0)),
-             ((0, 0, 0), (5, 5, 5), (0.5, -5, 0.5), (0, 1, 0)),
-             ((0, 0, 0), (5, 5, 5), (0.5, 0.5, 0.5), _norm([1, 1, 0]))]
+    # random rays on odd grids: the slab test and the kernels' DDA vs the oracle
+    cases = []
     for _ in range(300):
         lo = rng.uniform(-3, 0, 3)
         hi = lo + rng.uniform(0.5, 4, 3)
         o = rng.uniform(-6, 6, 3)
         tgt = rng.uniform(lo, hi)
         cases.append((lo, hi, o, _norm(tgt - o)))
+    # axis-parallel rays, rays starting inside, grazing a face
+    cases += [((0, 0, 0), (2, 3, 1), (0.5, 0.5, 0.5), (1, 0, 0)),
+              ((0, 0, 0), (2, 3, 1), (1.0, 1.5, 0.5), (0, 0, -1)),
+              ((0, 0, 0), (2, 3, 1), (-1, 0.0, 0.5), _norm([1, 0, 0]))]
     n = len(cases)
     inp = np.array([list(a) + list(b) + list(c) + list(d) for a, b, c, d in cases], np.float32)
     res = np.array([5, 7, 3], np.uint32)
     outb = native.probe(native.PROBE_BBOX, inp, n, (n, 2))
-    outd = native.probe(native.PROBE_DDA, inp, n, (n, 1 + 4 * 64), aux=res)
+    outd = native.probe(native.PROBE_DDA, inp, n, (n, native.DDA_PROBE_WIDTH), aux=res)
+    walked = 0
     for i, (lo, hi, o, d) in enumerate(cases):
         h, t = oracle_mod.bbox_ray(lo, hi, o, d)
         assert bool(outb[i, 0]) == h
         if h:
             assert np.float32(outb[i, 1]) == np.float32(t)
-        r = (5, 5, 5) if i < 4 else tuple(res)
-        if i < 4:
-            continue   # DDA probe uses res (5,7,3); the KAT grids are covered by the oracle tests
-        tr = oracle_mod.grid_trace(lo, hi, r, o, d, 64)
+        tr = oracle_mod.grid_trace(lo, hi, tuple(res), o, d, 64)
         if tr is None:
             assert outd[i, 0] == -1
             continue
         first, cells, ts = tr
         k = int(outd[i, 0])
-        assert k == len(ts)
-        got = outd[i, 1:1 + 4 * k].reshape(k, 4)
+        assert k == len(ts), (i, k)                     # -2 would flag a bad linear index
+        assert tuple(int(x) for x in outd[i, 1:4]) == tuple(int(x) for x in first)
+        got = outd[i, 4:4 + 4 * k].reshape(k, 4)
         assert np.array_equal(got[:, :3].astype(np.uint32), cells)
         assert np.array_equal(got[:, 3].astype(np.float32), ts)
+        walked += 1
+    assert walked > 100
 
 
 def test_probe_to_rgb_exp_log(oracle_mod, rng):
@@ -184,18 +235,18 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 
 
 # The timed kernels (no counting build) against the oracle on every scene:
-# the default wavefront path (XCD split with region queues), without the
-# split, with the split on the primary launch only, with packed counters, the
-# split organisation and the megakernel.
-MODES = [("wf", {}), ("wf", {"ZRT_XCD": "0"}), ("wf", {"ZRT_XCD": "1"}), ("wf", {"ZRT_CTR": "1"}),
-         ("split", {}), ("mega", {})]
+# wf_kernel (per-lane walk), the park kernel on the bounce launches or on
+# every launch, and the park schedule at its extremes (a test round as soon
+# as one lane parks / only when all 64 have; refill per lane / per wave).
+MODES = [("wf", {}), ("park-bounces", {"ZRT_PARK": "2"}), ("park-all", {"ZRT_PARK": "1"}),
+         ("park-eager", {"ZRT_PARK": "1", "ZRT_PARK_T": "1", "ZRT_PARK_R": "1"}),
+         ("park-lazy", {"ZRT_PARK": "1", "ZRT_PARK_T": "64", "ZRT_PARK_R": "64"})]
 
 
-@pytest.mark.parametrize("mode,env", MODES, ids=lambda m: str(m))
+@pytest.mark.parametrize("mode,env", MODES, ids=[m for m, _ in MODES])
 @pytest.mark.parametrize("name,camname,w,h,spp", CASES)
 def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mode, env, name, camname,
                                          w, h, spp):
-    monkeypatch.setenv("ZRT_MODE", mode)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     soup = scenes.get_scene(name)
@@ -211,43 +262,35 @@ def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mo
     assert res["stats"]["segments"] == int(ctr[0])
 
 
-# per-item pass bytes of each kernel organisation (render.hip: per_item)
-PER_ITEM = {"mega": 16, "wf": 96 + 16 + 32 * 4, "split": 96 + 16 + 16 + 32 * 4}
-
-
-@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
-def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode):
-    """Pass splits (sample ranges), rank splits (tile sets) and the three kernel
-    organisations (fused wavefront / split wavefront / megakernel) all give the
-    same image."""
+@pytest.mark.parametrize("mode,env", MODES[:3], ids=[m for m, _ in MODES[:3]])
+def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode, env):
+    """Pass splits (sample ranges), rank splits (tile sets), the timed kernels
+    and the counting megakernel all give the same image."""
     soup = scenes.get_scene("cornell")
     cam = camera_for(soup, None, 96, 80)
     rs = gpu_scenes("cornell")
-    monkeypatch.setenv("ZRT_MODE", "mega")
-    ref, _ = rs.render(cam, num_samples=6, max_bounce=4)
-    monkeypatch.setenv("ZRT_MODE", mode)
-    per_item = PER_ITEM[mode]
-    monkeypatch.setenv("ZRT_PASS_BYTES", str(per_item * 96 * 80 * 2))   # 2 samples per pass
-    monkeypatch.setenv("ZRT_WF_BYTES", str(per_item * 96 * 80 * 2))
-    multi, r2 = rs.render(cam, num_samples=6, max_bounce=4)
-    assert r2["stats"]["trace_launches"] == (3 if mode == "mega" else 3 * 4)
+    ref, _ = rs.render(cam, num_samples=6, max_bounce=4, stats=True)     # counting build
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    multi, r2 = rs.render(cam, num_samples=6, max_bounce=4, samples_per_pass=2)
+    assert r2["stats"]["trace_launches"] == 3 * 4
     assert np.array_equal(ref, multi)
-    monkeypatch.delenv("ZRT_PASS_BYTES")
-    monkeypatch.delenv("ZRT_WF_BYTES")
     img = np.zeros_like(ref)
     for r in range(3):
         rs.render(cam, img=img, num_samples=6, max_bounce=4, rank=r, num_ranks=3)
     assert np.array_equal(ref, img)
 
 
-@pytest.mark.parametrize("mode", ["wf", "split", "mega"])
-@pytest.mark.parametrize("mb", [0, 1, 5, 9, 17])
-def test_render_max_bounce_variants(oracle_mod, gpu_scenes, monkeypatch, mode, mb):
-    monkeypatch.setenv("ZRT_MODE", mode)
+@pytest.mark.parametrize("mode,env", MODES[:3] + [("counting", {})], ids=[m for m, _ in MODES[:3]] + ["counting"])
+@pytest.mark.parametrize("mb", [0, 1, 5, 9, 17, 32])
+def test_render_max_bounce_variants(oracle_mod, gpu_scenes, monkeypatch, mode, env, mb):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     soup = scenes.get_scene("cornell")
     c = soup.camera()
     cam = camera_for(soup, None, 40, 40)
-    img, res = gpu_scenes("cornell").render(cam, num_samples=2, max_bounce=mb, linear=True)
+    img, res = gpu_scenes("cornell").render(cam, num_samples=2, max_bounce=mb, linear=True,
+                                            stats=mode == "counting")
     ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, 40, 40)
     rgb, lin, _ = oracle_mod.OracleScene(soup).render(ocam, 2, mb, oracle_mod.RNG_PATH, 0, 16)
     assert np.array_equal(img.reshape(-1, 3), rgb)
@@ -267,5 +310,5 @@ def test_render_rejects_bad_config(gpu_scenes):
     with pytest.raises(native.ZrtError):
         gpu_scenes("sphere").render(cam, num_samples=0)
     with pytest.raises(native.ZrtError) as e:
-        gpu_scenes("sphere").render(cam, num_samples=1, max_bounce=65)
+        gpu_scenes("sphere").render(cam, num_samples=1, max_bounce=33)
     assert e.value.status == -5

@@ -17,8 +17,27 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the timed wf_kernel instantiations (render.hip: kWfMinWaves0 primary, kWfMinWaves bounces)
-TIMED = ["wf_kernelILi2ELi7ELb1ELb0EE", "wf_kernelILi2ELi6ELb0ELb0EE"]
+BUNDLE = "hipv4-amdgcn-amd-amdhsa--gfx950"
+
+
+def timed():
+    """The timed kernel instantiations, as libzrt reports them
+    (zrt_timed_kernels: built from the same constants render.hip launches)."""
+    sys.path.insert(0, ROOT)
+    from zig_raytracing_contest_amd import native
+    return native.timed_kernels()
+
+
+def has_gfx950(obj):
+    """True if the object's offload bundle holds a gfx950 code object."""
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fatbin")
+        if subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj,
+                           os.path.join(d, "x.o")], capture_output=True).returncode != 0:
+            return False
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--list", "--type=o", f"--input={fb}"],
+                           capture_output=True, text=True)
+        return r.returncode == 0 and BUNDLE in r.stdout
 
 
 def disassemble(obj):
@@ -27,7 +46,7 @@ def disassemble(obj):
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj,
                         os.path.join(d, "x.o")], check=True)
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}",
+                        f"--targets={BUNDLE}", f"--input={fb}",
                         f"--output={co}"], check=True)
         return subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True,
                               capture_output=True, text=True).stdout
@@ -69,7 +88,7 @@ def walk_spills(ins):
 
 def main():
     obj = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build", "obj", "render.o")
-    want = sys.argv[2:] or TIMED
+    want = sys.argv[2:] or timed()
     ks = kernels(disassemble(obj))
     bad = 0
     for w in want:

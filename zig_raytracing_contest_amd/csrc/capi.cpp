@@ -1,12 +1,29 @@
 // capi.cpp -- host-side C ABI helpers: status strings, camera (stage1),
 // ziggurat tables, the per-rank tile order of the packed image.
+#include <sched.h>
+
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "zrt_internal.h"
 
 using namespace zrt;
+
+namespace zrt {
+unsigned host_threads() {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) n = (unsigned)CPU_COUNT(&set);
+    if (const char* e = getenv("OMP_NUM_THREADS")) {
+        const int k = atoi(e);
+        if (k > 0) n = std::min(n, (unsigned)k);
+    }
+    return n;
+}
+}  // namespace zrt
 
 extern "C" const char* zrt_error_string(int s) {
     switch (s) {

@@ -21,6 +21,10 @@
 #include "../../include/zrt.h"
 #include "json.h"
 
+namespace zrt {
+unsigned host_threads();   // capi.cpp: CPUs this process may use, capped by OMP_NUM_THREADS
+}
+
 extern "C" int zrt_png_write(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h);
 
 namespace {
@@ -166,7 +170,7 @@ int main(int argc, char** argv) {
     if (!load_config("config.json", &cfg, &err)) { fprintf(stderr, "error: %s\n", err.c_str()); return 1; }
     info("Num samples: " + std::to_string(cfg.num_samples) + ", max bounce " + std::to_string(cfg.max_bounce));
     const uint32_t num_threads = cfg.num_threads >= 0 ? (uint32_t)cfg.num_threads
-                                                      : std::max(1u, std::thread::hardware_concurrency());
+                                                      : zrt::host_threads();
     info("Num threads: " + std::to_string(num_threads));
 
     // GPUs

@@ -70,7 +70,7 @@ extern "C" int zrt_geometry_build(const float* positions, const float* normals,
         geo->ncells = (uint32_t)ncells64;
 
         // SAT binning on host threads (stage2.zig:59-79 / 104-124)
-        unsigned nt = num_threads ? num_threads : std::max(1u, std::thread::hardware_concurrency());
+        unsigned nt = num_threads ? num_threads : host_threads();
         nt = std::min<unsigned>(nt, 64);
         const uint32_t nchunks = std::min<uint32_t>(n, nt * 8);
         std::vector<Chunk> chunks(nchunks);

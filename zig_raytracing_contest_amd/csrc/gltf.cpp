@@ -262,7 +262,7 @@ int load_images(Loader& L, uint32_t nthreads, std::vector<Image8>* images) {
                                                                       : png_decode(data, len, &(*images)[i]);
         }
     };
-    const size_t nt = std::max<size_t>(1, std::min<size_t>(nthreads ? nthreads : std::thread::hardware_concurrency(), n));
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(nthreads ? nthreads : host_threads(), n));
     std::vector<std::thread> th;
     for (size_t t = 1; t < nt; ++t) th.emplace_back(work, t, nt);
     work(0, nt);

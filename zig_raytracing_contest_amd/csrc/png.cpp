@@ -232,7 +232,7 @@ int png_encode_rgb(const uint8_t* rgb, int w, int h, int level, std::vector<uint
     // stream: any inflater (and stbi) reads it; only the file bytes differ
     // from a one-thread deflate (each piece starts with an empty window).
     const size_t row = rb + 1;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned hw = zrt::host_threads();
     const size_t min_piece = 256 * 1024;
     size_t np = std::min<size_t>(std::min<size_t>(hw, 32), std::max<size_t>(1, raw.size() / min_piece));
     np = std::min<size_t>(np, (size_t)h);

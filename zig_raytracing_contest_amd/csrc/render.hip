@@ -1,28 +1,23 @@
-// render.hip -- the render hot path on CDNA4 (gfx950): persistent path-trace
-// kernel + in-order sample resolve, behind the C ABI of include/zrt.h.
+// render.hip -- the render hot path on CDNA4 (gfx950): wavefront path-trace
+// kernels + in-order sample resolve, behind the C ABI of include/zrt.h.
 //
 // Reference: Scene.render / renderWorker / traceRayRecursive / traceRay
 // (src/stage3.zig:152-256) over Grid.traceRay + Iterator.next
 // (src/linalg.zig:443-496) and Triangle.rayIntersection (linalg.zig:696-722).
 //
-// Work decomposition (MI355X-first, not the reference's thread blocks):
+// Organisation (MI355X-first, not the reference's thread blocks):
 //   * a work item is ONE path sample (pixel, sample); items are numbered
 //     sample-major over this rank's packed pixel list (64x64 tiles walked in
 //     8x8 blocks, so one wave64 = one 8x8 pixel block of one sample index:
 //     coherent primary rays);
-//   * a persistent grid (CUs x resident blocks) pulls 64-item chunks from one
-//     atomic counter per pass, one returning atomic per wave (dequeue row of
-//     the MI355X price list: far below the ~100 us a chunk takes);
-//   * each lane traces its path iteratively (recursion -> loop) and keeps the
-//     per-bounce (emissive, albedo) pairs in registers, folding them back to
-//     front at the end: e0 + a0*(e1 + a1*(...)) is the recursion's exact
-//     arithmetic, so the radiance is bit-identical to traceRayRecursive;
-//   * each sample radiance is written to HBM (float4, coalesced 1 KiB per wave
-//     instruction) and a resolve kernel sums a pixel's samples IN SAMPLE ORDER
-//     (renderWorker's `pixel = pixel.add(ray_color)`), scales by the f32
-//     reciprocal of spp and quantizes with toRGB.  The round trip costs
-//     32 B/sample of HBM traffic (~3 ms for cfg3's 531M samples at 6 TB/s)
-//     and buys order-independent scheduling with an exact result.
+//   * bounce k of every path of a pass is one launch over a compacted queue
+//     of the paths still alive (wavefront organisation); each lane traces one
+//     Scene.traceRay segment and shades it (traceRayRecursive's body);
+//   * the per-bounce (emissive, albedo) pairs go to HBM planes and the resolve
+//     kernel folds them back to front per sample, then sums the samples IN
+//     SAMPLE ORDER (renderWorker's `pixel = pixel.add(ray_color)`), scales by
+//     the f32 reciprocal of spp and quantizes with toRGB: the image is
+//     bit-identical to the recursion's for any scheduling.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,7 +25,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
-#include <unordered_map>
 #include <vector>
 
 #include "zrt_internal.h"
@@ -53,9 +47,11 @@ using namespace zrt;
 namespace {
 
 constexpr float kFltEps = 1.1920928955078125e-07f;   // std.math.floatEps(f32)
-constexpr int kBlock = 256;                          // resolve / probes
-constexpr int kTraceBlock = 512;                     // launch bound; launched with trace_block()
+constexpr int kBlock = 256;                          // resolve / probes / helpers
+constexpr int kTraceBlock = 512;                     // launch bound of wf_kernel / trace_kernel
+constexpr int kTraceThreads = 256;                   // threads per wf_kernel / trace_kernel block
 constexpr int kTriBatch = 2;                         // triangle loads in flight per lane
+constexpr int kParkBlock = 1024;                     // wf_park_kernel: one workgroup per CU
 
 struct TraceParams {
     float bmin[3], bmax[3];
@@ -77,17 +73,15 @@ struct TraceParams {
     uint32_t total;           // items in this pass
     uint32_t max_bounce;
     uint64_t seed;
-    float4* out;              // total
+    float4* out;              // counting build: sample radiance per item
     uint32_t* counter;
-    unsigned long long* stats;   // segments, cells, tests, hits | profile
+    unsigned long long* stats;   // segments, cells, tests, hits, diagnostics
 };
 
-// Per-bounce (emissive, albedo) pairs of one path.  The fold reads them back
-// to front: e0 + a0*(e1 + a1*(...)) is traceRayRecursive's arithmetic
-// (stage3.zig:219); pass-through bounces (stage3.zig:212) add no pair.  The
-// array is indexed by the bounce slot at run time, so it lives in scratch
-// memory: it is written once per scatter and read once per path, never in
-// the traversal loop, and keeping it out of VGPRs buys waves per SIMD.
+// Per-bounce (emissive, albedo) pairs of one path (counting megakernel only).
+// The fold reads them back to front: e0 + a0*(e1 + a1*(...)) is
+// traceRayRecursive's arithmetic (stage3.zig:219); pass-through bounces
+// (stage3.zig:212) add no pair.
 template <int N>
 struct Stack {
     float e[3 * N], a[3 * N];
@@ -116,9 +110,6 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
-__device__ __forceinline__ bool dda_setup(const TraceParams& p, v3 o, v3 d, Dda& s) {
-    return dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s);
-}
 // Grid constants as wave-uniform registers (see GridK).
 __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     GridK g;
@@ -130,34 +121,19 @@ __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     return g;
 }
 
-// Mailbox of the last 4 triangle shapes tested by this ray segment.  The
-// bake copies a triangle into every cell it overlaps (5.6 copies each on the
-// contest stand-in), so a ray walking along a large triangle re-tests the
-// same vertices cell after cell.  A re-test cannot change the result:
-// acceptance depends only on t (nearest > t && t > 0, stage3.zig:172) and t
-// only on the vertices and the ray; if the first test set nearest = t the
-// re-test fails nearest > t, if it failed it fails again (nearest only
-// shrinks).  So a ref whose shape id (tri_pos[3j].w: equal positions ->
-// equal id, assigned at context creation) is in the mailbox is skipped.
-struct Mailbox {
-    uint32_t m0, m1, m2, m3;
-    __device__ __forceinline__ void reset() { m0 = m1 = m2 = m3 = 0xFFFFFFFFu; }
-    __device__ __forceinline__ bool has(uint32_t id) const { return id == m0 || id == m1 || id == m2 || id == m3; }
-    __device__ __forceinline__ void push(uint32_t id) { m3 = m2; m2 = m1; m1 = m0; m0 = id; }
-};
+__device__ __forceinline__ bool first_active_lane() {
+    return (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1));
+}
 
 // All triangles of one cell in reference order (stage3.zig:164-178), TB at
 // a time: the TB loads are issued before the first test so their latencies
 // overlap (one memory round trip per TB triangles instead of per triangle).
-// MB: mailbox skipping (see Mailbox); the counting build (STATS) tests every
-// ref as the reference does and only counts the ones MB would skip.
-template <int TB, bool STATS, bool MB = false>
+template <int TB, bool STATS>
 __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
                                           float& nearest, float& hu, float& hv, uint32_t& hidx,
-                                          uint32_t& n_tests, uint64_t* wstat, Mailbox& mbx) {
+                                          uint32_t& n_tests, uint64_t* wstat) {
     for (uint32_t i = b; i < e; i += TB) {
-        // counting build: wave trips of this loop (first active lane counts)
-        if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++wstat[1];
+        if (STATS && first_active_lane()) ++wstat[1];   // wave trips of this loop
         float4 A[TB], B[TB], Cc[TB];
 #pragma unroll
         for (int k = 0; k < TB; ++k) {
@@ -168,15 +144,7 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
         }
 #pragma unroll
         for (int k = 0; k < TB; ++k) {
-            bool live = i + (uint32_t)k < e;
-            if (MB || STATS) {
-                const uint32_t id = __float_as_uint(A[k].w);
-                const bool seen = mbx.has(id);
-                (void)seen;
-                if (MB) live = live && !seen;
-                if (live) mbx.push(id);
-            }
-            if (live) {
+            if (i + (uint32_t)k < e) {
                 if (STATS) ++n_tests;
                 float t, u, v;
                 if (tri_ray(mk(A[k].x, A[k].y, A[k].z), mk(B[k].x, B[k].y, B[k].z),
@@ -188,46 +156,37 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
     }
 }
 
-// Diagnostic build only (ZRT_PROFILE=1): s_memtime stamps apportion each
-// wave's cycles to code regions.  Never in the timed kernel.
-__device__ __forceinline__ uint64_t stamp() {
-    uint64_t t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-
 // Scene.traceRay (stage3.zig:152-186) with empty-space skipping that changes
 // nothing in the result: the DDA arithmetic runs for every cell exactly as
 // Iterator.next does; only the 8-byte Cell load is skipped when the cell's
 // brick holds no triangle (its range would be empty).
-template <bool STATS, bool PROF, int TB, bool MB = false>
+// STATS (counting build): n_cells / n_tests per lane; prof[] per wave:
+// [6] cell loads, [7] non-empty cells, [8] wave trips of the cell loop,
+// [9] wave trips of the triangle-batch loop, [10] cell trips with any test,
+// [4] 64-wide rounds if each trip's tests were shared evenly.
+template <bool STATS, int TB>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr) {
     float nearest = kInf;
-    Mailbox mbx;
-    mbx.reset();
     Dda s;
-    if (!dda_setup(p, o, d, s)) return nearest;
+    if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s)) return nearest;
     const uint32_t sh = p.occ_shift;
     const GridK gk = grid_consts(p);
     bool occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
     for (;;) {
-        uint64_t ta = 0, tb = 0;
-        if (PROF) ta = stamp();
         if (STATS) ++n_cells;
-        if (STATS && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1))) ++prof[8];
+        if (STATS && first_active_lane()) ++prof[8];
         uint32_t ncell = 0;
         if (occupied) {
             const uint2 cell = p.cells[s.lin];
             if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; ncell = cell.y - cell.x; }
-            test_cell<TB, STATS, MB>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8, mbx);
+            test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8);
         }
         if (STATS) {
             // wave-shared work of this trip: sum of the lanes' triangle counts
-            // -> trips with any test, and 64-wide rounds if shared evenly
             uint32_t* wc = wcnt + 2 * (threadIdx.x >> 6);
-            const bool first = (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1));
+            const bool first = first_active_lane();
             if (first) wc[0] = 0;
             __builtin_amdgcn_wave_barrier();
             atomicAdd(&wc[0], ncell);
@@ -238,129 +197,11 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                 prof[4] += (N + 63) / 64;
             }
         }
-        if (PROF) tb = stamp();
         bool crossed;
         float t_exit;
         DDA_STEP(s, gk, sh, crossed, t_exit);
         if (nearest <= t_exit) break;                      // stage3.zig:179-182
         if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
-        if (PROF) { const uint64_t tc = stamp(); prof[0] += tb - ta; prof[1] += tc - tb; }
-    }
-    return nearest;
-}
-
-// Scene.traceRay for the 64 rays of a wave, walked in lockstep, with the
-// triangle tests of each step shared across the wave.
-//
-// Per-lane testing (trace_ray) runs a wave's triangle loop as long as its
-// busiest lane: on the contest scene a wave trip that tests anything tests
-// 26 (ref, ray) pairs on average, yet costs 3 two-triangle trips (the max
-// over lanes), i.e. ~7% of the lanes do useful work.  Here, each step:
-//  1. every walking lane loads its cell's range [b, b+n) (if its brick is
-//     occupied);
-//  2. the wave lays all pairs (owner lane, ref) out in lane order - owner i
-//     covers pair slots [off_i, off_i + n_i) - and tests them 64 at a time,
-//     lane q taking pair slot r + q (one MT test per lane per round);
-//  3. each owner's winner is the lexicographic min of (t, ref index) over its
-//     pairs with 0 < t < nearest (an LDS 64-bit atomicMin on t's bits: t > 0
-//     orders like its bit pattern), which is exactly the first ref of the
-//     cell (stage3.zig:164-178 order) reaching the smallest accepted t, i.e.
-//     what the sequential `nearest > t && t > 0` loop keeps; the winner's
-//     lane also leaves (u, v) in LDS;
-//  4. every walking lane steps its DDA and applies the break (stage3.zig:179).
-// All lanes of the wave execute the loop (lanes without a ray pass alive =
-// false), so the cross-lane steps run converged.  LDS per wave: the rays
-// (o, nearest before the step | d, ref base) and the (key, u, v) slots.
-struct WaveLds {
-    float4 ray[128];               // [2*lane]: o.xyz, nearest0; [2*lane+1]: d.xyz, unused
-    unsigned long long best[64];   // per owner: (t bits << 32) | ref
-    float2 uv[64];
-    uint32_t base[64];             // per owner: ref of pair slot 0 (b - off, mod 2^32)
-};
-
-__device__ __forceinline__ float trace_wave(const TraceParams& p, const uint32_t* occ, WaveLds& L, bool alive,
-                                            v3 o, v3 d, float& hu, float& hv, uint32_t& hidx) {
-    const uint32_t lane = threadIdx.x & 63u;
-    float nearest = kInf;
-    hu = hv = 0.0f;
-    hidx = 0;
-    Dda s;
-    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
-    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
-    bool active = alive && dda_setup(p, o, d, s);
-    const uint32_t sh = p.occ_shift;
-    const GridK gk = grid_consts(p);
-    bool occupied = active && brick_occupied(p, occ, s.c0, s.c1, s.c2);
-    while (__ballot(active) != 0ull) {
-        uint32_t b = 0, n = 0;
-        if (active && occupied) {
-            const uint2 cell = p.cells[s.lin];
-            b = cell.x;
-            n = cell.y - cell.x;
-        }
-        const uint64_t own = __ballot(n != 0u);
-        if (own != 0ull) {
-            uint32_t my_off = 0, N = 0;
-            for (uint64_t m = own; m != 0ull; m &= m - 1ull) {      // scalar: owners in lane order
-                const uint32_t i = (uint32_t)__builtin_ctzll(m);
-                if (lane == i) my_off = N;
-                N += (uint32_t)__builtin_amdgcn_readlane((int)n, (int)i);
-            }
-            L.ray[2 * lane] = make_float4(o.x, o.y, o.z, nearest);
-            L.ray[2 * lane + 1] = make_float4(d.x, d.y, d.z, 0.0f);
-            L.base[lane] = b - my_off;
-            L.best[lane] = ~0ull;
-            __builtin_amdgcn_wave_barrier();
-            // workers: the lanes the compiler keeps enabled here (it may mask
-            // lanes whose walk has ended), numbered densely
-            const uint64_t ex = __ballot(1);
-            const uint32_t W = (uint32_t)__popcll(ex);
-            const uint32_t wi = (uint32_t)__popcll(ex & (lane ? (~0ull >> (64u - lane)) : 0ull));
-            for (uint32_t r = 0; r < N; r += W) {
-                const uint32_t q = r + wi;
-                uint32_t owner = 0, acc = 0;
-                for (uint64_t m = own; m != 0ull; m &= m - 1ull) {
-                    const uint32_t i = (uint32_t)__builtin_ctzll(m);
-                    const uint32_t ni = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)i);
-                    if (acc + ni > r && acc < r + W) owner = (q >= acc && q < acc + ni) ? i : owner;
-                    acc += ni;
-                }
-                const bool valid = q < N;
-                const float4 ra = L.ray[2 * owner], rb = L.ray[2 * owner + 1];
-                const uint32_t j = L.base[owner] + q;
-                bool cand = false;
-                float t = 0.0f, u = 0.0f, v = 0.0f;
-                if (valid) {
-                    const float4 A = p.tri_pos[3 * j + 0], B = p.tri_pos[3 * j + 1], C = p.tri_pos[3 * j + 2];
-                    cand = tri_ray(mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z), mk(ra.x, ra.y, ra.z),
-                                   mk(rb.x, rb.y, rb.z), &t, &u, &v) &&
-                           ra.w > t && t > 0.0f;
-                }
-                const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
-                if (cand) atomicMin(&L.best[owner], key);
-                __builtin_amdgcn_wave_barrier();
-                if (cand && L.best[owner] == key) L.uv[owner] = make_float2(u, v);
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (n != 0u) {
-                const unsigned long long k = L.best[lane];
-                if (k != ~0ull) {
-                    nearest = __uint_as_float((uint32_t)(k >> 32));
-                    hidx = (uint32_t)k;
-                    const float2 uv = L.uv[lane];
-                    hu = uv.x;
-                    hv = uv.y;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (active) {
-            bool crossed;
-            float t_exit;
-            DDA_STEP(s, gk, sh, crossed, t_exit);
-            if (nearest <= t_exit) active = false;                 // stage3.zig:179-182
-            else if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
-        }
     }
     return nearest;
 }
@@ -388,207 +229,6 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
         x += ((unsigned long long)hi << 32) | lo;
     }
     return x;
-}
-
-// The path-trace kernel: renderWorker's per-sample body (stage3.zig:237-241)
-// + traceRayRecursive (stage3.zig:188-220) made iterative.
-template <int MAXB, bool STATS, bool PROF, int TB, int MINW>
-__global__ __launch_bounds__(kTraceBlock, MINW) void trace_kernel(const TraceParams p) {
-    __shared__ double s_zig[514];
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    // cell+tris, dda, trace, shade, fetch, total (PROF); cell loads, non-empty cells (STATS)
-    // + wave trips of the cell loop / triangle-batch loop (STATS)
-    // [10]: trips with any test (STATS; was mailbox counts), [4]: shared rounds (STATS)
-    uint64_t prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    __shared__ uint32_t s_wcnt[2 * (kTraceBlock / 64)];
-    const uint64_t t_begin = PROF ? stamp() : 0;
-    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
-    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
-    __syncthreads();
-    const double* zx = s_zig;
-    const double* zf = s_zig + 257;
-
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
-
-    for (;;) {
-        const uint64_t t_fetch = PROF ? stamp() : 0;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(p.counter, 64u);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= p.total) break;
-        const uint32_t item = base + lane;
-        if (item >= p.total) continue;
-
-        const uint32_t s_local = item / p.P;
-        const uint32_t q = item - s_local * p.P;
-        const uint32_t pixel = p.pixlist[q];
-        const uint32_t py = pixel / p.w;
-        const uint32_t px = pixel - py * p.w;
-        Rng rng;
-        rng.s = path_key(p.seed, pixel, p.s0 + s_local);
-        // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35)
-        const float jx = rng_float(rng);
-        const float jy = rng_float(rng);
-        v3 o = mk(p.org[0], p.org[1], p.org[2]);
-        v3 d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
-                                 scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
-                             scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
-        Stack<MAXB> stk;
-        stk.init();
-        v3 L = mk(0, 0, 0);
-        uint32_t slot = 0;
-        if (PROF) prof[4] += stamp() - t_fetch;
-        for (uint32_t depth = p.max_bounce; depth > 0; --depth, ++slot) {
-            ++n_seg;
-            float hu = 0.0f, hv = 0.0f;
-            uint32_t hidx = 0;
-            const uint64_t t_tr = PROF ? stamp() : 0;
-            const float t = trace_ray<STATS, PROF, TB>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof,
-                                                       s_wcnt);
-            const uint64_t t_sh = PROF ? stamp() : 0;
-            if (PROF) prof[2] += t_sh - t_tr;
-            if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
-            if (STATS) ++n_hits;
-            // stage3.zig:199-206
-            const float4* tdp = p.tri_data + 4ull * hidx;
-            const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
-            const float w0 = 1.0f - hu - hv;
-            const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
-            const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
-            const DevMat& m = p.mats[__float_as_uint(d3.w)];
-            const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
-            const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
-            const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
-            const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
-                               scale(mk(d1.z, d1.w, d2.x), hv));
-            const v3 no = add(o, scale(d, t + kFltEps));        // ray.at(hit.t + eps)
-            if (!(rng_float(rng) > transparency)) {             // stage3.zig:207
-                // randomUnitVector (linalg.zig:140-148): 3 x floatNorm, normalize
-                const float nx = (float)rng_norm64(rng, zx, zf);
-                const float ny = (float)rng_norm64(rng, zx, zf);
-                const float nz = (float)rng_norm64(rng, zx, zf);
-                d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
-                stk.set(slot, emissive, albedo);                // stage3.zig:214-219
-            }                                                   // else pass-through :208-212
-            o = no;
-            if (PROF) prof[3] += stamp() - t_sh;
-        }
-        L = stk.fold(L);
-        p.out[item] = make_float4(L.x, L.y, L.z, 0.0f);
-    }
-    if (PROF) {
-        prof[5] = stamp() - t_begin;
-        if (lane == 0)
-            for (int k = 0; k < 6; ++k) atomicAdd(&p.stats[8 + k], (unsigned long long)prof[k]);
-    }
-    const unsigned long long s0 = wave_sum(n_seg);
-    unsigned long long s1 = 0, s2 = 0, s3 = 0;
-    unsigned long long s4 = 0, s5 = 0;
-    if (STATS) {
-        s1 = wave_sum(n_cells); s2 = wave_sum(n_tests); s3 = wave_sum(n_hits);
-        s4 = wave_sum(prof[6]); s5 = wave_sum(prof[7]);
-        const unsigned long long s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]), s8 = wave_sum(prof[10]);
-        const unsigned long long s9 = wave_sum(prof[4]);
-        if (lane == 0) {
-            atomicAdd(&p.stats[6], s6); atomicAdd(&p.stats[7], s7); atomicAdd(&p.stats[14], s8);
-            atomicAdd(&p.stats[15], s9);
-        }
-    }
-    if (lane == 0) {
-        atomicAdd(&p.stats[0], s0);
-        if (STATS) {
-            atomicAdd(&p.stats[1], s1);
-            atomicAdd(&p.stats[2], s2);
-            atomicAdd(&p.stats[3], s3);
-            atomicAdd(&p.stats[4], s4);
-            atomicAdd(&p.stats[5], s5);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Wavefront mode: one launch per bounce over a compacted queue of live paths.
-//
-// The megakernel above keeps a lane on one path from camera to sky, so a
-// wave lives as long as its longest path (most waves hold a 4-segment path
-// while the mean is ~1.9: about half the lanes idle at the path level).  Here
-// bounce k is its own launch over the paths still alive after bounce k-1:
-// every lane traces exactly one segment and shades it; a continuing path is
-// appended to the next queue (one returning atomic per wave, ballot + mbcnt
-// ranks), a finished one stores its terminal radiance (env / 0) and the mask
-// of bounce slots that scattered.  The per-bounce (emissive, albedo) pairs go
-// to HBM in [slot][item] planes and the resolve kernel folds them back to
-// front per sample, then sums the samples in order: the arithmetic of
-// traceRayRecursive and renderWorker, bit for bit.
-//
-// A queue record is 48 B: (o.xyz, item) (d.xyz, depth | slot << 16)
-// (rng lo, rng hi, mask, 0).
-struct WfParams {
-    TraceParams t;
-    const float4* q_in;
-    const uint32_t* n_in;     // live paths in q_in (written by the previous launch)
-    float4* q_out;
-    uint32_t* n_out;
-    uint32_t* fetch;          // work counter of this launch
-    float4* stk;              // [(slot*2 + {0:e,1:a}) * T + item]
-    float4* term;             // [item]: terminal L.xyz, scatter mask bits
-    float4* hit;              // split mode: [queue index] (t, u, v, tri) of this bounce
-    uint32_t T;               // items in this pass
-    uint32_t refill;          // split mode: idle lanes before a wave fetches rays
-    uint32_t* hist;           // ray sort: per-key counts of the appended paths (null: no sort)
-    uint32_t sort_bits;       // ray sort: origin-region bits per axis
-    // XCD split (wf_kernel): 8 block groups, one per XCD; the queue is cut into
-    // 8 regions, region g holding the paths of pixel range g (capacity S*Pg)
-    uint32_t xcd;             // 0: one queue, one counter
-    uint32_t* fetch8;         // work counter per group of this launch
-    uint32_t ctr;             // region counter stride (u32)
-    const uint32_t* n_in8;    // paths per region of q_in
-    uint32_t* n_out8;         // paths per region of q_out
-};
-
-// Work / append counters: `ctr` u32 apart (32: one per 128-byte line, so the
-// waves' atomics on different counters do not queue on one line; 1: packed).
-constexpr uint32_t kCtrMax = 32;
-
-// XCD split: first pixel (packed order) of group g, 8x8-block aligned.
-__device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
-    const uint32_t nblk = (P + 63u) >> 6;
-    return min(P, (nblk * g / 8u) * 64u);
-}
-
-// Ray-sort key of a continuing path: the origin's region in a 2^R per axis
-// subdivision of the grid bbox (Morton order), then the direction octant.
-// Paths of one key start close together heading the same way, so a wave of
-// them walks overlapping cells and tests the same triangles (coalesced
-// loads, similar walk lengths).
-__device__ __forceinline__ uint32_t sort_key(const TraceParams& p, v3 o, v3 d, uint32_t R) {
-    const float n = (float)(1u << R);
-    uint32_t r[3];
-    const float oc[3] = {o.x, o.y, o.z};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float f = (oc[a] - p.bmin[a]) / (p.bmax[a] - p.bmin[a]) * n;
-        r[a] = f > 0.0f ? min((uint32_t)f, (1u << R) - 1u) : 0u;   // NaN -> 0
-    }
-    uint32_t m = 0;
-    for (uint32_t b = 0; b < R; ++b)
-        m |= (((r[0] >> b) & 1u) << (3 * b)) | (((r[1] >> b) & 1u) << (3 * b + 1)) |
-             (((r[2] >> b) & 1u) << (3 * b + 2));
-    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    return (m << 3) | oct;
-}
-
-// Count one key per lane of `live` into hist, one atomic per distinct key
-// of the wave.
-__device__ __forceinline__ void wave_key_count(uint32_t* hist, bool live, uint32_t key) {
-    uint64_t pend = __ballot(live);
-    while (pend) {
-        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(pend));
-        const uint64_t m = __ballot(live && key == k);
-        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(pend)) atomicAdd(&hist[k], (uint32_t)__popcll(m));
-        pend &= ~m;
-    }
 }
 
 // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35) for
@@ -619,9 +259,147 @@ __device__ __forceinline__ Rng camera_rng(const TraceParams& p, uint32_t item) {
     return rng;
 }
 
+// The counting megakernel: renderWorker's per-sample body (stage3.zig:237-241)
+// + traceRayRecursive (stage3.zig:188-220) made iterative, one lane = one
+// path from camera to sky, with exact per-lane work counters (segments,
+// cells, triangle tests, hits).  Same RNG -> same paths as the timed
+// wavefront kernels, so its counts are the timed frame's algorithmic work
+// (bench.py's roofline) and the parity tests' traversal counters.
+template <int MAXB>
+__global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams p) {
+    __shared__ double s_zig[514];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
+    uint64_t prof[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __shared__ uint32_t s_wcnt[2 * (kTraceBlock / 64)];
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
+    __syncthreads();
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
+
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(p.counter, 64u);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= p.total) break;
+        const uint32_t item = base + lane;
+        if (item >= p.total) continue;
+
+        Rng rng;
+        v3 o, d;
+        camera_ray(p, item, rng, o, d);
+        Stack<MAXB> stk;
+        stk.init();
+        v3 L = mk(0, 0, 0);
+        uint32_t slot = 0;
+        for (uint32_t depth = p.max_bounce; depth > 0; --depth, ++slot) {
+            ++n_seg;
+            float hu = 0.0f, hv = 0.0f;
+            uint32_t hidx = 0;
+            const float t = trace_ray<true, kTriBatch>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof,
+                                                       s_wcnt);
+            if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
+            ++n_hits;
+            // stage3.zig:199-206
+            const float4* tdp = p.tri_data + 4ull * hidx;
+            const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
+            const float w0 = 1.0f - hu - hv;
+            const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
+            const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
+            const DevMat& m = p.mats[__float_as_uint(d3.w)];
+            const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
+            const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
+            const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
+            const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
+                               scale(mk(d1.z, d1.w, d2.x), hv));
+            const v3 no = add(o, scale(d, t + kFltEps));        // ray.at(hit.t + eps)
+            if (!(rng_float(rng) > transparency)) {             // stage3.zig:207
+                // randomUnitVector (linalg.zig:140-148): 3 x floatNorm, normalize
+                const float nx = (float)rng_norm64(rng, zx, zf);
+                const float ny = (float)rng_norm64(rng, zx, zf);
+                const float nz = (float)rng_norm64(rng, zx, zf);
+                d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+                stk.set(slot, emissive, albedo);                // stage3.zig:214-219
+            }                                                   // else pass-through :208-212
+            o = no;
+        }
+        L = stk.fold(L);
+        p.out[item] = make_float4(L.x, L.y, L.z, 0.0f);
+    }
+    const unsigned long long s0 = wave_sum(n_seg), s1 = wave_sum(n_cells), s2 = wave_sum(n_tests),
+                             s3 = wave_sum(n_hits), s4 = wave_sum(prof[6]), s5 = wave_sum(prof[7]),
+                             s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]), s8 = wave_sum(prof[10]),
+                             s9 = wave_sum(prof[4]);
+    if (lane == 0) {
+        atomicAdd(&p.stats[0], s0);
+        atomicAdd(&p.stats[1], s1);
+        atomicAdd(&p.stats[2], s2);
+        atomicAdd(&p.stats[3], s3);
+        atomicAdd(&p.stats[4], s4);
+        atomicAdd(&p.stats[5], s5);
+        atomicAdd(&p.stats[6], s6);
+        atomicAdd(&p.stats[7], s7);
+        atomicAdd(&p.stats[14], s8);
+        atomicAdd(&p.stats[15], s9);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wavefront organisation: one launch per bounce over a compacted queue of
+// live paths.
+//
+// A megakernel keeps a lane on one path from camera to sky, so a wave lives
+// as long as its longest path.  Here bounce k is its own launch over the
+// paths still alive after bounce k-1: every lane traces one segment and
+// shades it; a continuing path is appended to the next queue (one returning
+// atomic per wave and region, ballot + popcount ranks), a finished one
+// stores its terminal radiance (env / 0) and the mask of bounce slots that
+// scattered.  The per-bounce (emissive, albedo) pairs go to HBM in
+// [slot][item] planes and wf_resolve_kernel folds them back to front.
+//
+// A queue record is 48 B: (o.xyz, item) (d.xyz, depth | slot << 16)
+// (rng lo, rng hi, mask, 0).
+//
+// XCD split: blocks are dispatched round-robin over the 8 XCDs, so block
+// group g = blockIdx % 8 shares one L2.  The packed pixel list is cut into 8
+// ranges (8x8-block aligned) and every queue into 8 regions, region g holding
+// the paths of pixel range g (capacity S * P_g).  Group g takes pixel range
+// g / region g first, then helps the other groups: a screen region's paths
+// stay on one XCD from bounce to bounce.  Same items, other order: same image.
+struct WfParams {
+    TraceParams t;
+    const float4* q_in;
+    float4* q_out;
+    float4* stk;              // [(slot*2 + {0:e,1:a}) * T + item]
+    float4* term;             // [item]: terminal L.xyz, scatter mask bits
+    uint32_t T;               // items in this pass
+    uint32_t* fetch8;         // work counter per group of this launch
+    const uint32_t* n_in8;    // paths per region of q_in
+    uint32_t* n_out8;         // paths per region of q_out
+    // wf_park_kernel: exact per-cell occupancy blob (see OccX) and schedule
+    const uint32_t* occx;
+    uint32_t occx_words, occx_nbw, occx_moff, occx_nb0, occx_nb01;
+    uint32_t test_min;        // parked lanes before a wave runs a test round
+    uint32_t refill_min;      // finished lanes before a wave shades and refills
+};
+
+// Work / append counters: one per 128-byte line (32 u32), so the waves'
+// atomics on different counters do not queue on one line (packed counters
+// made the region queues 2.4x slower, round 1).
+constexpr uint32_t kCtr = 32;
+
+// XCD split: first pixel (packed order) of group g, 8x8-block aligned.
+__device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
+    const uint32_t nblk = (P + 63u) >> 6;
+    return min(P, (nblk * g / 8u) * 64u);
+}
+
 // traceRayRecursive's body after the hit (stage3.zig:195-219) for one
 // segment: env colour on a miss, else material lookup, (e, a) pair to the
-// bounce stack on a scatter, pass-through otherwise.  Returns true when the
+// bounce planes on a scatter, pass-through otherwise.  Returns true when the
 // path continues (o, d, depth, slot, rng, mask updated); false with L set
 // when it terminates.
 __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* zx, const double* zf,
@@ -658,48 +436,87 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
     return depth != 0;                                      // depth 0: recursion returns 0
 }
 
-// Append the wave's continuing paths to the next queue: one returning atomic
-// per wave, ranks from ballot + popcount.  XCD split: to the region of the
-// wave's pixel group `reg` (all 64 items of a fetch come from one region).
-__device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d,
-                                         uint32_t item, uint32_t depth, uint32_t slot, const Rng& rng,
-                                         uint32_t mask, uint32_t reg = 0) {
-    const uint64_t bal = __ballot(cont);
-    if (!bal) return;
-    if (w.n_out8) {
-        const uint32_t S = w.t.total / max(w.t.P, 1u);
+__device__ __forceinline__ void q_store(const WfParams& w, uint32_t pos, v3 o, v3 d, uint32_t item, uint32_t depth,
+                                        uint32_t slot, const Rng& rng, uint32_t mask) {
+    w.q_out[3ull * pos] = make_float4(o.x, o.y, o.z, __uint_as_float(item));
+    w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
+    w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s), __uint_as_float((uint32_t)(rng.s >> 32)),
+                                          __uint_as_float(mask), 0.0f);
+}
+
+// Append the continuing paths of the wave (lanes with `cont`) to the next
+// queue, each to the region `reg` of its pixel range: one returning atomic
+// per distinct region of the wave, ranks from ballot + popcount.
+__device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d, uint32_t item,
+                                          uint32_t depth, uint32_t slot, const Rng& rng, uint32_t mask,
+                                          uint32_t reg) {
+    const uint32_t S = w.t.total / max(w.t.P, 1u);
+    uint64_t pend = __ballot(cont);
+    while (pend) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)reg, (int)lead);
+        const uint64_t m = __ballot(cont && reg == g);
         uint32_t ob = 0;
-        if ((threadIdx.x & 63u) == 0) ob = atomicAdd(&w.n_out8[reg * w.ctr], (uint32_t)__popcll(bal));
-        ob = __builtin_amdgcn_readfirstlane(ob) + S * xcd_q0(w.t.P, reg);
-        if (cont) {
-            const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
-            w.q_out[3ull * pos] = make_float4(o.x, o.y, o.z, __uint_as_float(item));
-            w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
-            w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s),
-                                                  __uint_as_float((uint32_t)(rng.s >> 32)),
-                                                  __uint_as_float(mask), 0.0f);
-        }
-        return;
-    }
-    uint32_t key = 0;
-    if (w.hist) {
-        key = cont ? sort_key(w.t, o, d, w.sort_bits) : 0u;
-        wave_key_count(w.hist, cont, key);
-    }
-    uint32_t ob = 0;
-    if ((threadIdx.x & 63u) == 0) ob = atomicAdd(w.n_out, (uint32_t)__popcll(bal));
-    ob = __builtin_amdgcn_readfirstlane(ob);
-    if (cont) {
-        const uint32_t pos = ob + (uint32_t)__popcll(bal & below);
-        w.q_out[3ull * pos] = make_float4(o.x, o.y, o.z, __uint_as_float(item));
-        w.q_out[3ull * pos + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(depth | (slot << 16)));
-        w.q_out[3ull * pos + 2] = make_float4(__uint_as_float((uint32_t)rng.s),
-                                              __uint_as_float((uint32_t)(rng.s >> 32)),
-                                              __uint_as_float(mask), __uint_as_float(key));
+        if ((threadIdx.x & 63u) == lead) ob = atomicAdd(&w.n_out8[g * kCtr], (uint32_t)__popcll(m));
+        ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)lead) + S * xcd_q0(w.t.P, g);
+        if (cont && reg == g) q_store(w, ob + (uint32_t)__popcll(m & below), o, d, item, depth, slot, rng, mask);
+        pend &= ~m;
     }
 }
 
-template <int TB, int MINW, bool PRIMARY, bool MB = false>
+// Fetch work for a wave from the XCD group queues, group `grp` first: one
+// returning atomic takes `want` consecutive entries of group grp's range
+// (primary launch: items of pixel range g for every sample of the pass;
+// bounce launches: region g of q_in).  Returns false once every group is
+// exhausted.  On true, entries [base, min(base + want, lim)) of group grp
+// belong to this wave; entry j maps to the item / queue index of ent_index().
+template <bool PRIMARY>
+__device__ __forceinline__ bool wf_fetch(const WfParams& w, uint32_t want, uint32_t& grp, uint32_t& tried,
+                                         uint32_t& base, uint32_t& lim) {
+    const TraceParams& p = w.t;
+    const uint32_t S = p.total / max(p.P, 1u);
+    for (;;) {
+        const uint32_t q0 = xcd_q0(p.P, grp);
+        const uint32_t pg = xcd_q0(p.P, grp + 1u) - q0;
+        lim = PRIMARY ? S * pg : w.n_in8[grp * kCtr];
+        uint32_t b = 0;
+        if ((threadIdx.x & 63u) == 0) b = atomicAdd(&w.fetch8[grp * kCtr], want);
+        base = __builtin_amdgcn_readfirstlane(b);
+        if (base < lim) return true;
+        if (++tried == 8u) return false;
+        grp = (grp + 1u) & 7u;
+    }
+}
+template <bool PRIMARY>
+__device__ __forceinline__ uint32_t ent_index(const TraceParams& p, uint32_t grp, uint32_t j) {
+    const uint32_t S = p.total / max(p.P, 1u);
+    const uint32_t q0 = xcd_q0(p.P, grp);
+    const uint32_t pg = xcd_q0(p.P, grp + 1u) - q0;
+    return PRIMARY ? (j / pg) * p.P + q0 + j % pg : S * q0 + j;
+}
+
+// The path state of queue entry / primary item `i` that shading needs.
+template <bool PRIMARY>
+__device__ __forceinline__ void path_state(const WfParams& w, uint32_t i, uint32_t& item, uint32_t& depth,
+                                           uint32_t& slot, Rng& rng, uint32_t& mask) {
+    if (PRIMARY) {
+        item = i;
+        depth = w.t.max_bounce;
+        slot = 0;
+        mask = 0;
+        rng = camera_rng(w.t, i);
+    } else {
+        const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+        item = __float_as_uint(a.w);
+        depth = __float_as_uint(b.w) & 0xFFFFu;
+        slot = __float_as_uint(b.w) >> 16;
+        rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+        mask = __float_as_uint(c.z);
+    }
+}
+
+// wf_kernel: one lane = one segment, walked and tested by the lane itself.
+template <int MINW, bool PRIMARY>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -711,43 +528,15 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const double* zf = s_zig + 257;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t n = PRIMARY ? p.total : *w.n_in;
     uint32_t n_seg = 0, dummy = 0;
-    // XCD split (w.xcd): blocks are dispatched round-robin over the 8 XCDs,
-    // so group g = blockIdx % 8 shares one L2.  Group g takes pixel range g
-    // (8x8-block aligned) for every sample of the pass, and in later bounces
-    // the queue region of those pixels' paths, then helps the other groups:
-    // a screen region's paths stay on one XCD from bounce to bounce.  Same
-    // items, other order: same image.
     uint32_t grp = blockIdx.x & 7u, tried = 0;
-    const uint32_t S = p.total / max(p.P, 1u);
 
     for (;;) {
-        uint32_t base = 0, i = 0, reg = 0;
-        bool valid;
-        if (w.xcd) {
-            uint32_t q0 = 0, pg = 0, lim = 0;
-            for (;;) {
-                q0 = xcd_q0(p.P, grp);
-                pg = xcd_q0(p.P, grp + 1u) - q0;
-                lim = PRIMARY ? S * pg : w.n_in8[grp * w.ctr];
-                if (lane == 0) base = atomicAdd(&w.fetch8[grp * w.ctr], 64u);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (base < lim || ++tried == 8u) break;
-                grp = (grp + 1u) & 7u;
-            }
-            if (tried == 8u) break;
-            reg = grp;
-            const uint32_t j = base + lane;
-            valid = j < lim;
-            i = !valid ? 0u : PRIMARY ? (j / pg) * p.P + q0 + j % pg : S * q0 + j;
-        } else {
-            if (lane == 0) base = atomicAdd(w.fetch, 64u);
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (base >= n) break;
-            i = base + lane;
-            valid = i < n;
-        }
+        uint32_t base = 0, lim = 0;
+        if (!wf_fetch<PRIMARY>(w, 64u, grp, tried, base, lim)) break;
+        const uint32_t j = base + lane;
+        const bool valid = j < lim;
+        const uint32_t i = valid ? ent_index<PRIMARY>(p, grp, j) : 0u;
         bool cont = false;
         uint32_t mask = 0, r_item = 0, r_depth = 0, r_slot = 0;
         v3 r_o = mk(0, 0, 0), r_d = mk(0, 0, 0);
@@ -771,20 +560,10 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             float t = kInf, hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
             if (depth != 0)
-                t = trace_ray<false, false, TB, MB>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
+                t = trace_ray<false, kTriBatch>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
             uint32_t item, slot;
             Rng rng;
-            if (PRIMARY) {
-                item = i;
-                slot = 0;
-                rng = camera_rng(p, i);
-            } else {
-                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
-                item = __float_as_uint(a.w);
-                slot = __float_as_uint(b.w) >> 16;
-                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-                mask = __float_as_uint(c.z);
-            }
+            path_state<PRIMARY>(w, i, item, depth, slot, rng, mask);
             v3 L = mk(0, 0, 0);
             if (depth != 0) {
                 ++n_seg;
@@ -793,270 +572,269 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
         }
-        wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask, reg);
+        wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask, grp);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
 }
 
-// wf_kernel with the wave-cooperative traversal (trace_wave).  Dynamic LDS:
-// the occupancy bits, then one WaveLds per wave.
-template <int MINW, bool PRIMARY>
-__global__ __launch_bounds__(kTraceBlock, MINW) void wf_wave_kernel(const WfParams w) {
+// ---------------------------------------------------------------------------
+// wf_park_kernel: Scene.traceRay as walk / park / test rounds with exact
+// per-cell occupancy in LDS (opt-in, ZRT_PARK=1, while it is measured).
+//
+// Counted on the contest stand-in (cfg3, round 1): a segment visits 85
+// cells, 4.3 of them non-empty, and tests 18.2 triangles; per wave the
+// per-lane triangle loop ran 134 two-triangle trips for 9.1 per lane (6.8%
+// of the lanes busy) and the walk 184 trips for 85 steps per lane.  Here:
+//  * the exact occupancy of every cell sits in LDS (OccX), so a lane loads a
+//    cell's [begin, end) only when the cell holds triangles, and the walk of
+//    empty cells is DDA arithmetic plus one LDS lookup per 4^3 brick entered;
+//  * a lane that reaches a non-empty cell issues the range load and PARKS
+//    (its load is in flight while the others walk on);
+//  * once `test_min` lanes are parked (or none walks) the wave runs one test
+//    round: the (parked lane, triangle) pairs of all parked lanes are laid
+//    out in lane order and tested 64 at a time, one pair per lane; each
+//    parked lane keeps the lexicographic min of (t, ref) over its pairs with
+//    0 < t < nearest -- exactly what the reference's in-order
+//    `nearest > t and t > 0` loop keeps (stage3.zig:164-178: the smallest t,
+//    the first ref among equal t; t > 0 orders like its bit pattern) -- and
+//    walks on from that cell;
+//  * finished lanes wait until `refill_min` of them are done, then shade
+//    together (traceRayRecursive's body, stage3.zig:195-219), append, and
+//    take fresh paths (persistent waves, dynamic fetch).
+// Per lane the cells, the tests, their order semantics and the break test
+// after every cell (stage3.zig:179-182) are the reference's: same hit.
+//
+// OccX (4^3-cell bricks): one bit per brick, the u16 number of occupied
+// bricks before each 32-brick word, one 64-bit cell mask per occupied brick
+// (+ one zero mask).
+struct OccX {
+    const uint32_t* bits;
+    const uint16_t* prefix;
+    const unsigned long long* masks;
+};
+__device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
+    const uint32_t wd = L.bits[b >> 5];
+    const uint32_t r = (uint32_t)L.prefix[b >> 5] + (uint32_t)__popc(wd & ((1u << (b & 31u)) - 1u));
+    const unsigned long long m = L.masks[r];            // r <= occupied count: the zero mask at worst
+    return ((wd >> (b & 31u)) & 1u) ? m : 0ull;
+}
+__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const Dda& s) {
+    return (s.c2 >> 2) * w.occx_nb01 + (s.c1 >> 2) * w.occx_nb0 + (s.c0 >> 2);
+}
+__device__ __forceinline__ uint32_t occx_bit(const Dda& s) {
+    return ((s.c2 & 3u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
+}
+
+// Per-wave LDS of the test rounds.
+struct ParkSlot {
+    float4 o[64];                    // lane's ray origin; w: nearest entering the round
+    float4 d[64];                    // lane's ray direction; w (bits): ref of its pair slot 0
+    unsigned long long best[64];     // per parked lane: (t bits << 32) | ref of its best pair
+    float2 uv[64];                   // (u, v) of that pair
+    uint32_t mark[64];               // lane + 1 of the parked lane whose pairs start at this slot
+};
+
+// Exclusive prefix sum over the wave (the whole wave must be active: every
+// DPP read below runs under full EXEC).  Row scans by DPP row_shr with
+// bound_ctrl (a source lane outside the row reads 0), rows joined through
+// their last lanes.  NOT written as `rl >= k ? dpp(x) : 0`: that puts the
+// DPP read under a partial EXEC, and gfx9 DPP treats a disabled source lane
+// as invalid (tools/dpp_probe.hip; the cause of round 1's park-mode fault).
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uint32_t& total) {
+    uint32_t s = x;
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x111, 0xf, 0xf, true);   // row_shr:1
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x112, 0xf, 0xf, true);   // row_shr:2
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xf, 0xf, true);   // row_shr:4
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xf, 0xf, true);   // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)s, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)s, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)s, 47);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)s, 63);
+    const uint32_t row = lane >> 4;
+    s += row == 0u ? 0u : (row == 1u ? r0 : (row == 2u ? r0 + r1 : r0 + r1 + r2));
+    total = r0 + r1 + r2 + r3;
+    return s - x;
+}
+
+template <bool PRIMARY>
+__global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ double s_zig[514];
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
+    for (uint32_t i = threadIdx.x; i < w.occx_words; i += blockDim.x) s_dyn[i] = w.occx[i];
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
-    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
     __syncthreads();
-    WaveLds& L = reinterpret_cast<WaveLds*>(s_occ + ((p.occ_words + 3u) & ~3u))[threadIdx.x >> 6];
+    OccX L;
+    L.bits = s_dyn;
+    L.prefix = reinterpret_cast<const uint16_t*>(s_dyn + w.occx_nbw);
+    L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + w.occx_moff);
+    ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + ((w.occx_words + 3u) & ~3u))[threadIdx.x >> 6];
     const double* zx = s_zig;
     const double* zf = s_zig + 257;
+
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t n = PRIMARY ? p.total : *w.n_in;
+    const uint32_t test_min = w.test_min, refill_min = w.refill_min;
+    const GridK gk = grid_consts(p);
+    constexpr uint32_t kIdle = 0, kWalk = 1, kPark = 2, kDone = 3;
+    uint32_t st = kIdle;
+    bool more = true;
+    uint32_t grp = blockIdx.x & 7u, tried = 0;
+    // the segment: ray, DDA state, current brick's cell mask, best hit, range
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+    Dda s;
+    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
+    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
+    unsigned long long bm = 0ull;
+    float nearest = kInf, hu = 0.0f, hv = 0.0f;
+    uint32_t hidx = 0, rb = 0, re = 0;
+    // the path: entry index (primary item / queue index) and its region
+    uint32_t qi = 0, reg = 0;
     uint32_t n_seg = 0;
 
     for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(w.fetch, 64u);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= n) break;
-        const uint32_t i = base + lane;
-        const bool valid = i < n;
-        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
-        Rng rng;
-        rng.s = 0;
-        v3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-        if (valid) {
-            if (PRIMARY) {
-                item = i;
-                camera_ray(p, item, rng, o, d);
-                depth = p.max_bounce;
-            } else {
-                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
-                o = mk(a.x, a.y, a.z);
-                item = __float_as_uint(a.w);
-                d = mk(b.x, b.y, b.z);
-                depth = __float_as_uint(b.w) & 0xFFFFu;
-                slot = __float_as_uint(b.w) >> 16;
-                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-                mask = __float_as_uint(c.z);
+        // ---- shade + refill round, once enough lanes are finished or idle
+        const uint64_t busy = __ballot(st == kWalk || st == kPark);
+        if ((uint32_t)(64 - __popcll(busy)) >= refill_min || busy == 0ull) {
+            if (__ballot(st == kDone) != 0ull) {
+                bool cont = false;
+                uint32_t item = 0, depth = 0, slot = 0, mask = 0;
+                Rng rng;
+                rng.s = 0;
+                if (st == kDone) {                                 // stage3.zig:195-219
+                    path_state<PRIMARY>(w, qi, item, depth, slot, rng, mask);
+                    ++n_seg;
+                    v3 Lr = mk(0, 0, 0);
+                    cont = shade_segment(w, zx, zf, item, nearest, hu, hv, hidx, o, d, depth, slot, rng, mask, Lr);
+                    if (!cont) w.term[item] = make_float4(Lr.x, Lr.y, Lr.z, __uint_as_float(mask));
+                    st = kIdle;
+                }
+                wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, reg);
             }
-        }
-        const bool alive = valid && depth != 0u;
-        float hu, hv;
-        uint32_t hidx;
-        const float t = trace_wave(p, s_occ, L, alive, o, d, hu, hv, hidx);
-        bool cont = false;
-        if (valid) {
-            v3 Lr = mk(0, 0, 0);
-            if (alive) {
-                ++n_seg;
-                cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, Lr);
-            }
-            if (!cont) w.term[item] = make_float4(Lr.x, Lr.y, Lr.z, __uint_as_float(mask));
-        }
-        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask);
-    }
-    const unsigned long long s0 = wave_sum(n_seg);
-    if (lane == 0) atomicAdd(&p.stats[0], s0);
-}
-
-// Split wavefront (default): bounce k = wf_trace_kernel (Scene.traceRay only)
-// + wf_shade_kernel (the rest of the segment, one lane per path).
-//
-// Traversal lengths within a wave differ by 10x or more (a ray grazing the
-// ground plane crosses 200 cells, one hitting the object next to it 3), so
-// a wave that traces 64 rays start to finish idles most lanes most of the
-// time.  Here the unit of work in the loop is ONE grid cell: a lane whose ray
-// has finished writes its hit record and goes idle, and once `refill` lanes
-// of the wave are idle they fetch fresh rays from the queue together (one
-// atomic per wave) while the others keep walking (persistent threads with
-// dynamic ray fetch).  The per-ray state is only the ray, the DDA state and
-// the best hit; shading lives in its own kernel so none of its registers
-// are live in the traversal loop.
-template <int TB, int MINW, bool PRIMARY>
-__global__ __launch_bounds__(kTraceBlock, MINW) void wf_trace_kernel(const WfParams w) {
-    const TraceParams& p = w.t;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_occ[];
-    for (uint32_t i = threadIdx.x; i < p.occ_words; i += blockDim.x) s_occ[i] = p.occ[i];
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t n = PRIMARY ? p.total : *w.n_in;
-    const uint32_t refill = w.refill;
-    const uint32_t sh = p.occ_shift;
-    const GridK gk = grid_consts(p);
-    bool active = false, occupied = false, more = n != 0;
-    uint32_t ray = 0, hidx = 0;
-    float nearest = kInf, hu = 0.0f, hv = 0.0f;
-    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    Dda s;
-    Mailbox mbx;
-    mbx.reset();
-    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
-    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (more && nidle >= refill) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(w.fetch, nidle);
-            base = __builtin_amdgcn_readfirstlane(base);
-            more = base < n && n - base > nidle;
-            if (!active) {
-                const uint32_t r = base + (uint32_t)__popcll(idle & below);
-                if (base < n && r < n) {
-                    ray = r;
-                    if (PRIMARY) {
-                        Rng rng;
-                        camera_ray(p, r, rng, o, d);
-                    } else {
-                        const float4 a = w.q_in[3ull * r], b = w.q_in[3ull * r + 1];
-                        o = mk(a.x, a.y, a.z);
-                        d = mk(b.x, b.y, b.z);
+            const uint64_t idle = __ballot(st == kIdle);
+            if (more && idle != 0ull) {
+                uint32_t base = 0, lim = 0;
+                more = wf_fetch<PRIMARY>(w, (uint32_t)__popcll(idle), grp, tried, base, lim);
+                if (more && st == kIdle) {
+                    const uint32_t j = base + (uint32_t)__popcll(idle & below);
+                    if (j < lim) {
+                        qi = ent_index<PRIMARY>(p, grp, j);
+                        reg = grp;
+                        uint32_t depth;
+                        if (PRIMARY) {
+                            Rng rng0;
+                            camera_ray(p, qi, rng0, o, d);
+                            depth = p.max_bounce;
+                        } else {
+                            const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
+                            o = mk(qa.x, qa.y, qa.z);
+                            d = mk(qb.x, qb.y, qb.z);
+                            depth = __float_as_uint(qb.w) & 0xFFFFu;
+                        }
+                        if (depth == 0u) {                         // max_bounce 0: black, nothing traced
+                            w.term[qi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        } else {
+                            nearest = kInf;
+                            hu = hv = 0.0f;
+                            hidx = 0;
+                            W.o[lane] = make_float4(o.x, o.y, o.z, 0.0f);
+                            W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
+                            if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s)) {   // stage3.zig:153-156
+                                bm = occx_mask(L, occx_brick(w, s));
+                                if ((bm >> occx_bit(s)) & 1ull) {
+                                    const uint2 c = p.cells[s.lin];
+                                    rb = c.x;
+                                    re = c.y;
+                                    st = kPark;
+                                } else {
+                                    st = kWalk;
+                                }
+                            } else {
+                                st = kDone;                        // misses the grid: nearest = +inf
+                            }
+                        }
                     }
-                    nearest = kInf;
-                    hu = hv = 0.0f;
-                    hidx = 0;
-                    mbx.reset();
-                    if (dda_setup(p, o, d, s)) {                   // stage3.zig:153-156
-                        active = true;
-                        occupied = brick_occupied(p, s_occ, s.c0, s.c1, s.c2);
-                    } else {
-                        w.hit[r] = make_float4(kInf, 0.0f, 0.0f, 0.0f);
+                }
+            }
+            if (__ballot(st != kIdle) == 0ull) {
+                if (!more) break;
+                continue;
+            }
+        }
+        // ---- walk until test_min lanes are parked or nobody walks
+        for (;;) {
+            const uint64_t wk = __ballot(st == kWalk);
+            if (wk == 0ull || (uint32_t)__popcll(__ballot(st == kPark)) >= test_min) break;
+            if (st == kWalk) {
+                bool crossed;
+                float t_exit;
+                DDA_STEP(s, gk, 2u, crossed, t_exit);
+                if (nearest <= t_exit) {                           // stage3.zig:179-182
+                    st = kDone;
+                } else {
+                    if (crossed) bm = occx_mask(L, occx_brick(w, s));
+                    if ((bm >> occx_bit(s)) & 1ull) {
+                        const uint2 c = p.cells[s.lin];
+                        rb = c.x;
+                        re = c.y;
+                        st = kPark;
                     }
                 }
             }
         }
-        if (__ballot(active) == 0) {
-            if (!more) break;
-            continue;
+        // ---- test round: the parked lanes' cells, all pairs over all lanes
+        if (__ballot(st == kPark) != 0ull) {
+            const uint32_t n = st == kPark ? re - rb : 0u;
+            uint32_t tot = 0;
+            const uint32_t off = wave_excl_sum(n, lane, tot);
+            W.o[lane].w = nearest;
+            W.d[lane].w = __uint_as_float(rb - off);
+            W.best[lane] = ~0ull;
+            uint32_t carry = 0;
+            for (uint32_t r = 0; r < tot; r += 64u) {
+                // owner of pair slot r + lane: the last parked lane starting
+                // at or before it (mark), or the one running over from r - 1
+                W.mark[lane] = 0u;
+                __builtin_amdgcn_wave_barrier();
+                if (n != 0u && off >= r && off < r + 64u) W.mark[off - r] = lane + 1u;
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t starts = __ballot(W.mark[lane] != 0u);
+                const uint64_t upto = starts & (~0ull >> (63u - lane));
+                const uint32_t owner = upto ? W.mark[63u - (uint32_t)__builtin_clzll(upto)] - 1u : carry;
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)owner, 63);
+                const uint32_t g = r + lane;
+                const float4 ro = W.o[owner], rd = W.d[owner];
+                const uint32_t j = __float_as_uint(rd.w) + g;
+                bool cand = false;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                if (g < tot) {
+                    const float4 A = p.tri_pos[3ull * j], B = p.tri_pos[3ull * j + 1], C = p.tri_pos[3ull * j + 2];
+                    cand = tri_ray_flat(mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z),
+                                        mk(ro.x, ro.y, ro.z), mk(rd.x, rd.y, rd.z), &t, &u, &v) &&
+                           ro.w > t && t > 0.0f;                   // stage3.zig:172
+                }
+                const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
+                if (cand) atomicMin(&W.best[owner], key);
+                __builtin_amdgcn_wave_barrier();
+                if (cand && W.best[owner] == key) W.uv[owner] = make_float2(u, v);
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (n != 0u) {
+                const unsigned long long k = W.best[lane];
+                if (k != ~0ull) {
+                    nearest = __uint_as_float((uint32_t)(k >> 32));
+                    hidx = (uint32_t)k;
+                    const float2 uv = W.uv[lane];
+                    hu = uv.x;
+                    hv = uv.y;
+                }
+            }
+            if (st == kPark) st = kWalk;                           // the cell is done: step out of it next
         }
-        if (active) {
-            if (occupied) {
-                const uint2 cell = p.cells[s.lin];
-                uint32_t nt = 0;
-                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, nt, nullptr, mbx);
-            }
-            bool crossed;
-            float t_exit;
-            DDA_STEP(s, gk, sh, crossed, t_exit);
-            if (nearest <= t_exit) {                               // stage3.zig:179-182
-                w.hit[ray] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
-                active = false;
-            } else if (crossed) {
-                occupied = brick_occupied(p, s_occ, s.c0, s.c1, s.c2);
-            }
-        }
-    }
-}
-
-template <bool PRIMARY>
-__global__ __launch_bounds__(kBlock) void wf_shade_kernel(const WfParams w) {
-    const TraceParams& p = w.t;
-    __shared__ double s_zig[514];
-    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
-    __syncthreads();
-    const double* zx = s_zig;
-    const double* zf = s_zig + 257;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t n = PRIMARY ? p.total : *w.n_in;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    uint32_t n_seg = 0;
-    for (uint32_t base = wave * 64u; base < n; base += nwaves * 64u) {
-        const uint32_t i = base + lane;
-        bool cont = false;
-        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
-        Rng rng;
-        rng.s = 0;
-        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-        if (i < n) {
-            if (PRIMARY) {
-                item = i;
-                camera_ray(p, item, rng, o, d);
-                depth = p.max_bounce;
-            } else {
-                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
-                o = mk(a.x, a.y, a.z);
-                item = __float_as_uint(a.w);
-                d = mk(b.x, b.y, b.z);
-                depth = __float_as_uint(b.w) & 0xFFFFu;
-                slot = __float_as_uint(b.w) >> 16;
-                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-                mask = __float_as_uint(c.z);
-            }
-            v3 L = mk(0, 0, 0);
-            if (depth != 0) {               // max_bounce 0: black, nothing traced
-                ++n_seg;
-                const float4 h = w.hit[i];
-                cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth,
-                                     slot, rng, mask, L);
-            }
-            if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
-        }
-        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
-}
-
-// Ray sort between bounces (counting sort on sort_key): exclusive scan of
-// the key counts into cursors (one block), then every record moves to its
-// key's range (one returning atomic per distinct key per wave).  The order
-// inside a key is arrival order; results do not depend on queue order (every
-// path writes only its own item's slots).
-__global__ __launch_bounds__(1024) void sort_scan_kernel(uint32_t* hist, uint32_t* cursor, uint32_t nbins) {
-    __shared__ uint32_t part[1024];
-    const uint32_t per = (nbins + 1023u) / 1024u;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < min(b0 + per, nbins); ++b) sum += hist[b];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024u; off <<= 1) {            // inclusive Hillis-Steele scan
-        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - sum;
-    for (uint32_t b = b0; b < min(b0 + per, nbins); ++b) {
-        cursor[b] = run;
-        run += hist[b];
-        hist[b] = 0;                                           // clean for the next bounce
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void sort_scatter_kernel(const float4* __restrict__ src, float4* dst,
-                                                              const uint32_t* n_in, uint32_t* cursor) {
-    const uint32_t n = *n_in;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t base = wave * 64u; base < n; base += nwaves * 64u) {
-        const uint32_t i = base + lane;
-        const bool live = i < n;
-        float4 a = make_float4(0, 0, 0, 0), b = a, c = a;
-        if (live) { a = src[3ull * i]; b = src[3ull * i + 1]; c = src[3ull * i + 2]; }
-        const uint32_t key = __float_as_uint(c.w);
-        uint64_t pend = __ballot(live);
-        uint32_t pos = 0;
-        while (pend) {
-            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(pend));
-            const uint64_t m = __ballot(live && key == k);
-            uint32_t ob = 0;
-            if (lane == (uint32_t)__builtin_ctzll(pend)) ob = atomicAdd(&cursor[k], (uint32_t)__popcll(m));
-            ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)__builtin_ctzll(pend));
-            if ((m >> lane) & 1ull) pos = ob + (uint32_t)__popcll(m & below);
-            pend &= ~m;
-        }
-        if (live) { dst[3ull * pos] = a; dst[3ull * pos + 1] = b; dst[3ull * pos + 2] = c; }
-    }
 }
 
 // Fold + ordered sample sum + toRGB for wavefront mode (stage3.zig:219,
@@ -1095,8 +873,9 @@ __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(const float4* __rest
     if (lin) { lin[3 * (size_t)q] = l.x; lin[3 * (size_t)q + 1] = l.y; lin[3 * (size_t)q + 2] = l.z; }
 }
 
-// renderWorker tail (stage3.zig:236-242): ordered per-pixel sum over this
-// pass's samples, then (last pass) * (1/spp) and toRGB.
+// renderWorker tail (stage3.zig:236-242) for the counting megakernel:
+// ordered per-pixel sum over this pass's samples, then (last pass) * (1/spp)
+// and toRGB.
 __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restrict__ out, uint32_t P,
                                                          uint32_t S, float4* acc, int first, int last,
                                                          float inv_spp, uint8_t* rgb, float* lin) {
@@ -1119,46 +898,27 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restric
 }
 
 using TraceFn = void (*)(const TraceParams);
+using WfFn = void (*)(const WfParams);
 
-// Timed kernel: launch bound (512 threads, 6 waves/SIMD) -> 80 VGPRs; the
-// few spills land outside the DDA loop and 6 waves hide more memory latency
-// than 5 unspilled ones (cfg3 at 32 spp: 1581 vs 1480 Mrays/s, r01 sweep).
-constexpr int kMinWaves = 6;
-// wf_kernel bounce launches: 6 waves/SIMD (80 VGPRs, 88 B/lane of spills
-// against 128 at 7).  Early r01 sweeps had 7 ahead by 1-2%, but 7 is at the
-// mercy of the spill allocator: the final r01 kernel at 7 ran cfg3 (256 spp)
-// at 1933 Mrays/s against 2108 at 6 on the same box, cfg5 678 vs 777, cfg2
-// 2005 vs 1968.  The primary launch (coherent rays, the larger share on
-// sparse scenes) keeps 7 (kWfMinWaves0): 2113-2114 on cfg3.  8 (64 VGPRs)
-// spills: 1503.
+// wf_kernel occupancy (waves per SIMD, __launch_bounds__): 6 for every
+// launch (80 VGPRs, no scratch access inside the cell walk).  7 waves put 2-3
+// spill reloads in the bounce walk and ran cfg3 at 1933 vs 2108 Mrays/s
+// (round 1); the 7-wave primary launch was within 0.2% of 6 in round 1 and
+// now reloads one spilled pair per cell step.  The timed instantiations are
+// exactly these two (tests/test_codegen.py reads them from zrt_timed_kernels).
 constexpr int kWfMinWaves = 6;
-constexpr int kWfMinWaves0 = 7;
-constexpr int kSplitMinWaves = 6;
+constexpr int kWfMinWaves0 = 6;
+const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true>;
+const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false>;
 
-template <int MAXB>
-TraceFn pick(bool stats, bool prof) {
-    if (prof) return (TraceFn)trace_kernel<MAXB, false, true, kTriBatch, 1>;
-    if (stats) return (TraceFn)trace_kernel<MAXB, true, false, kTriBatch, 1>;
-    return (TraceFn)trace_kernel<MAXB, false, false, kTriBatch, kMinWaves>;
-}
-
-// Threads per trace block: a multiple of 64, at most the launch bound.
-int trace_block() {
-    int b = 256;
-    if (const char* e = getenv("ZRT_TRACE_BLOCK")) b = atoi(e);
-    b = std::max(64, std::min(kTraceBlock, b / 64 * 64));
-    return b;
-}
-
-// max_bounce picks the stack depth the kernel is compiled for.
-TraceFn trace_fn(uint32_t max_bounce, bool stats, bool prof) {
-    if (max_bounce <= 4) return pick<4>(stats, prof);
-    if (max_bounce <= 8) return pick<8>(stats, prof);
-    if (max_bounce <= 16) return pick<16>(stats, prof);
-    if (max_bounce <= 32) return pick<32>(stats, prof);
+// max_bounce picks the stack depth the counting kernel is compiled for.
+TraceFn count_fn(uint32_t max_bounce) {
+    if (max_bounce <= 4) return (TraceFn)trace_kernel<4>;
+    if (max_bounce <= 8) return (TraceFn)trace_kernel<8>;
+    if (max_bounce <= 16) return (TraceFn)trace_kernel<16>;
+    if (max_bounce <= 32) return (TraceFn)trace_kernel<32>;
     return nullptr;
 }
-
 
 struct DeviceGuard {
     int prev = -1;
@@ -1182,6 +942,12 @@ int grow(T** p, size_t* cap, size_t n) {
     return ZRT_OK;
 }
 
+// OccX (wf_park_kernel): LDS left for the blob in one 1024-thread workgroup
+// per CU after the per-wave ParkSlots and the static ziggurat tables.
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
+constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - 256;
+
 }  // namespace
 
 struct zrt_context {
@@ -1191,7 +957,6 @@ struct zrt_context {
     std::vector<hipEvent_t> ev_trace;
     zrt_grid grid{};
     uint32_t ncells = 0, nrefs = 0, nmat = 0;
-    bool has_ids = false;            // tri_pos w holds shape ids (ZRT_MB=1 at creation)
     uint2* d_cells = nullptr;
     float4* d_pos = nullptr;
     float4* d_data = nullptr;
@@ -1200,16 +965,16 @@ struct zrt_context {
     double* d_zig = nullptr;
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
+    uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
+    uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
+    bool occx_ok = false;
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
-    float4* d_out = nullptr; size_t out_cap = 0;
+    float4* d_out = nullptr; size_t out_cap = 0;     // counting build
     float4* d_q0 = nullptr; size_t q0_cap = 0;       // wavefront queues
     float4* d_q1 = nullptr; size_t q1_cap = 0;
     float4* d_term = nullptr; size_t term_cap = 0;
     float4* d_stk = nullptr; size_t stk_cap = 0;
-    float4* d_hit = nullptr; size_t hit_cap = 0;
-    uint32_t* d_hist = nullptr; size_t hist_cap = 0;     // ray sort
-    uint32_t* d_cursor = nullptr; size_t cursor_cap = 0;
     uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
@@ -1268,6 +1033,18 @@ extern "C" int zrt_device_count(int* count) {
     return ZRT_OK;
 }
 
+// The timed wf_kernel instantiations, as the substrings of their mangled
+// names that tools/spill_check.py / tests/test_codegen.py look for in the
+// gfx950 code object (primary launch, then bounce launches).  No HIP call.
+extern "C" const char* zrt_timed_kernels(void) {
+#define ZRT_STR2(x) #x
+#define ZRT_STR(x) ZRT_STR2(x)
+    static_assert(kWfMinWaves0 == 6 && kWfMinWaves == 6, "update the strings below");
+    return "wf_kernelILi" ZRT_STR(6) "ELb1EE,wf_kernelILi" ZRT_STR(6) "ELb0EE";
+#undef ZRT_STR
+#undef ZRT_STR2
+}
+
 // Start-up work of the first GPU call, done ahead: the device's context and
 // the library's code objects (one fat binary, loaded on first use: ~0.1-0.2 s
 // on MI355X).  Lets a host overlap it with file loading.
@@ -1286,8 +1063,9 @@ extern "C" int zrt_device_warmup(int device) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_pix,
-                    c->d_out, c->d_q0, c->d_q1, c->d_term, c->d_stk, c->d_hit, c->d_hist, c->d_cursor, c->d_wfc, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
+    void* bufs[] = {c->d_cells, c->d_pos,  c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ,
+                    c->d_occx,  c->d_pix,  c->d_out,  c->d_q0,   c->d_q1,     c->d_term, c->d_stk,
+                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -1297,41 +1075,65 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     delete c;
 }
 
-// Shape id per ref for the mailbox: refs with bit-identical (v0, e1, e2)
-// share an id (the bake's per-cell copies of one triangle, and any
-// coincident triangles, whose tests are identical too).
-static std::vector<uint32_t> shape_ids(const float* pos, uint32_t n) {
-    struct Key { uint32_t w[9]; bool operator==(const Key& o) const { return !memcmp(w, o.w, sizeof w); } };
-    struct Hash {
-        size_t operator()(const Key& k) const {
-            uint64_t h = 0x9E3779B97F4A7C15ull;
-            for (uint32_t x : k.w) h = (h ^ x) * 0xBF58476D1CE4E5B9ull, h ^= h >> 29;
-            return (size_t)h;
+namespace {
+
+// OccX on the device, pass 1: one thread per 4^3 brick -> its 64-bit cell
+// mask (bit (z&3)<<4 | (y&3)<<2 | (x&3) = cell non-empty) and the brick bit.
+__global__ __launch_bounds__(kBlock) void occx_mask_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                           uint32_t r2, uint32_t nb0, uint32_t nb1, uint32_t nb,
+                                                           unsigned long long* __restrict__ masks,
+                                                           uint32_t* __restrict__ bits) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    unsigned long long m = 0ull;
+    if (b < nb) {
+        const uint32_t bx = b % nb0, by = (b / nb0) % nb1, bz = b / (nb0 * nb1);
+        for (uint32_t k = 0; k < 64; ++k) {
+            const uint32_t x = bx * 4 + (k & 3u), y = by * 4 + ((k >> 2) & 3u), z = bz * 4 + (k >> 4);
+            if (x < r0 && y < r1 && z < r2) {
+                const uint2 c = cells[((uint64_t)z * r1 + y) * r0 + x];
+                if (c.x < c.y) m |= 1ull << k;
+            }
         }
-    };
-    std::unordered_map<Key, uint32_t, Hash> ids;
-    ids.reserve(n);
-    std::vector<uint32_t> out(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        Key k;
-        memcpy(k.w, pos + 9ull * i, sizeof k.w);
-        out[i] = ids.emplace(k, (uint32_t)ids.size()).first->second;
+        masks[b] = m;
     }
-    return out;
+    const uint64_t bal = __ballot(b < nb && m != 0ull);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (b < nb && (lane == 0 || lane == 32)) bits[b >> 5] = (uint32_t)(bal >> lane);
 }
 
-// Brick occupancy of the cells on the device (device-built contexts).
-__global__ __launch_bounds__(kBlock) void occ_bits_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
-                                                          uint32_t ncells, uint32_t sh, uint32_t nb0, uint32_t nb1,
-                                                          uint32_t* __restrict__ bits) {
-    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
-        const uint2 c = cells[ci];
-        if (!(c.x < c.y)) continue;
-        const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / (r0 * r1);
-        const uint32_t b = ((z >> sh) * nb1 + (y >> sh)) * nb0 + (x >> sh);
-        atomicOr(&bits[b >> 5], 1u << (b & 31u));
+// Pass 2 (one block): u16 prefix of occupied bricks per 32-brick word, the
+// occupied masks compacted in brick order, then the zero mask; out[0] = the
+// number of occupied bricks.
+__global__ __launch_bounds__(1024) void occx_pack_kernel(const uint32_t* __restrict__ bits, uint32_t nbw,
+                                                         const unsigned long long* __restrict__ masks,
+                                                         uint16_t* __restrict__ prefix,
+                                                         unsigned long long* __restrict__ packed,
+                                                         uint32_t* __restrict__ out) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nbw + 1023u) / 1024u;
+    const uint32_t w0 = threadIdx.x * per, w1 = min(w0 + per, nbw);
+    uint32_t sum = 0;
+    for (uint32_t wd = w0; wd < w1; ++wd) sum += (uint32_t)__popc(bits[wd]);
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {            // inclusive Hillis-Steele scan
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t wd = w0; wd < w1; ++wd) {
+        prefix[wd] = (uint16_t)min(run, 0xFFFFu);
+        for (uint32_t wb = bits[wd]; wb; wb &= wb - 1u) packed[run++] = masks[32u * wd + (uint32_t)__builtin_ctz(wb)];
+    }
+    if (threadIdx.x == 1023) {
+        packed[run] = 0ull;
+        out[0] = run;
     }
 }
+
+}  // namespace
 
 static int context_base(zrt_context* c) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1357,16 +1159,9 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
     std::vector<float4> pos(3 * nr), dat(4 * nr);
-    // shape ids (tri_pos w) only for the opt-in mailbox variant: the hash over
-    // every ref costs tens of ms of context creation (the CLI's wall clock)
-    c->has_ids = getenv("ZRT_MB") && atoi(getenv("ZRT_MB")) == 1;
-    const std::vector<uint32_t> shape = c->has_ids ? shape_ids(s->triangles_pos, c->nrefs)
-                                                   : std::vector<uint32_t>(c->nrefs, 0u);
     for (uint32_t i = 0; i < c->nrefs; ++i) {
         const float* q = s->triangles_pos + 9ull * i;
-        float idf;
-        memcpy(&idf, &shape[i], 4);
-        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], idf);
+        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], 0.0f);
         pos[3 * i + 1] = make_float4(q[3], q[4], q[5], 0.0f);
         pos[3 * i + 2] = make_float4(q[6], q[7], q[8], 0.0f);
         float tmp[16];
@@ -1409,52 +1204,95 @@ static int context_materials(zrt_context* c, const zrt_scene* s) {
     return ZRT_OK;
 }
 
-// Brick occupancy from the host cells, or (host_cells null) from c->d_cells
-// on the device; then the work counters.
+// OccX blob layout for nb bricks (nbw 32-brick words) and `occupied` masks:
+// bits | u16 prefix per word | (8-byte aligned) masks + the zero mask.
+static void occx_layout(uint64_t nbw, uint64_t occupied, uint64_t* moff, uint64_t* words) {
+    const uint64_t pw = (nbw + 1) / 2;                   // prefix words
+    *moff = (nbw + pw + 1) & ~1ull;
+    *words = *moff + 2 * (occupied + 1);
+}
+
+// Brick occupancy (4^3-cell bricks: 4 KB of bits for a 128^3 grid, round 1's
+// best) and OccX, from the host cells or (host_cells null) from c->d_cells on
+// the device; then the work counters.
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
-    // brick occupancy bitmap: smallest power-of-two brick whose bitmap fits
-    // the LDS budget (ZRT_OCC_BYTES, default 32 KiB; ZRT_OCC_SHIFT forces it)
-    {
-        size_t budget = 4096;   // 4^3-cell bricks for a 128^3 grid (measured best, r01)
-        if (const char* e = getenv("ZRT_OCC_BYTES")) budget = (size_t)atoll(e);
-        int forced = -1;
-        if (const char* e = getenv("ZRT_OCC_SHIFT")) forced = atoi(e);
-        const uint32_t* r = c->grid.resolution;
-        uint32_t sh = 0;
-        for (;; ++sh) {
-            const uint64_t nb = (uint64_t)((r[0] + (1u << sh) - 1) >> sh) * ((r[1] + (1u << sh) - 1) >> sh) *
-                                ((r[2] + (1u << sh) - 1) >> sh);
-            const uint64_t bytes = (nb + 31) / 32 * 4;
-            if (sh >= 16) break;
-            if (bytes > 65536) continue;   // never more than 64 KiB of LDS per block
-            if ((forced >= 0 && (int)sh >= forced) || (forced < 0 && bytes <= budget)) break;
-        }
-        c->occ_shift = sh;
-        for (int i = 0; i < 3; ++i) c->occ_nb[i] = (r[i] + (1u << sh) - 1) >> sh;
-        const uint64_t nb = (uint64_t)c->occ_nb[0] * c->occ_nb[1] * c->occ_nb[2];
-        c->occ_words = (uint32_t)((nb + 31) / 32);
-        std::vector<uint32_t> bits(std::max<uint32_t>(c->occ_words, 1), 0u);
-        HIP_TRY(hipMalloc((void**)&c->d_occ, bits.size() * 4));
-        if (host_cells) {
-            for (uint32_t z = 0; z < r[2]; ++z)
-                for (uint32_t y = 0; y < r[1]; ++y)
-                    for (uint32_t x = 0; x < r[0]; ++x) {
-                        const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
-                        if (host_cells[2 * ci] < host_cells[2 * ci + 1]) {
-                            const uint64_t b =
-                                ((uint64_t)(z >> sh) * c->occ_nb[1] + (y >> sh)) * c->occ_nb[0] + (x >> sh);
-                            bits[b >> 5] |= 1u << (b & 31);
-                        }
+    const uint32_t* r = c->grid.resolution;
+    const uint32_t sh = 2;
+    c->occ_shift = sh;
+    for (int i = 0; i < 3; ++i) c->occ_nb[i] = (r[i] + (1u << sh) - 1) >> sh;
+    const uint64_t nb = (uint64_t)c->occ_nb[0] * c->occ_nb[1] * c->occ_nb[2];
+    if (nb > (1ull << 24)) return ZRT_ERR_UNSUPPORTED;    // > 64 KB of brick bits: more than LDS holds
+    const uint64_t nbw = (nb + 31) / 32;
+    c->occ_words = (uint32_t)nbw;
+    for (int i = 0; i < 3; ++i) c->occx_nb[i] = c->occ_nb[i];
+    HIP_TRY(hipMalloc((void**)&c->d_occ, nbw * 4));
+    if (host_cells) {
+        std::vector<unsigned long long> mask(nb, 0ull);
+        for (uint32_t z = 0; z < r[2]; ++z)
+            for (uint32_t y = 0; y < r[1]; ++y)
+                for (uint32_t x = 0; x < r[0]; ++x) {
+                    const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
+                    if (host_cells[2 * ci] < host_cells[2 * ci + 1]) {
+                        const uint64_t b = ((uint64_t)(z >> 2) * c->occ_nb[1] + (y >> 2)) * c->occ_nb[0] + (x >> 2);
+                        mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
                     }
-            HIP_TRY(hipMemcpy(c->d_occ, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
-        } else {
-            HIP_TRY(hipMemsetAsync(c->d_occ, 0, bits.size() * 4, c->stream));
-            hipLaunchKernelGGL(occ_bits_kernel, dim3(std::min<uint32_t>((c->ncells + kBlock - 1) / kBlock, 8192)),
-                               dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells, sh, c->occ_nb[0],
-                               c->occ_nb[1], c->d_occ);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipStreamSynchronize(c->stream));
+                }
+        std::vector<uint32_t> bits(nbw, 0u);
+        std::vector<uint16_t> prefix(nbw, 0);
+        std::vector<unsigned long long> masks;
+        uint64_t run = 0;
+        for (uint64_t wd = 0; wd < nbw; ++wd) {
+            prefix[wd] = (uint16_t)std::min<uint64_t>(run, 0xFFFF);
+            for (uint64_t b = wd * 32; b < std::min<uint64_t>(nb, wd * 32 + 32); ++b)
+                if (mask[b]) { bits[wd] |= 1u << (b & 31); masks.push_back(mask[b]); ++run; }
         }
+        masks.push_back(0ull);
+        HIP_TRY(hipMemcpy(c->d_occ, bits.data(), nbw * 4, hipMemcpyHostToDevice));
+        uint64_t moff, words;
+        occx_layout(nbw, run, &moff, &words);
+        c->occx_ok = run < 0xFFFF && words * 4 <= kOccxBudget;
+        if (c->occx_ok) {
+            std::vector<uint32_t> blob(words, 0u);
+            memcpy(blob.data(), bits.data(), nbw * 4);
+            memcpy(blob.data() + nbw, prefix.data(), nbw * 2);
+            memcpy(blob.data() + moff, masks.data(), masks.size() * 8);
+            c->occx_words = (uint32_t)words;
+            c->occx_nbw = (uint32_t)nbw;
+            c->occx_moff = (uint32_t)moff;
+            HIP_TRY(hipMalloc((void**)&c->d_occx, words * 4));
+            HIP_TRY(hipMemcpy(c->d_occx, blob.data(), words * 4, hipMemcpyHostToDevice));
+        }
+    } else {
+        // the blob for the largest possible occupancy, then the real size
+        uint64_t moff, words;
+        occx_layout(nbw, nb, &moff, &words);
+        unsigned long long* d_masks = nullptr;
+        uint32_t* d_blob = nullptr;
+        uint32_t* d_n = nullptr;
+        HIP_TRY(hipMalloc((void**)&d_masks, nb * 8));
+        HIP_TRY(hipMalloc((void**)&d_blob, words * 4));
+        HIP_TRY(hipMalloc((void**)&d_n, 4));
+        c->d_occx = d_blob;            // freed with the context from here on
+        HIP_TRY(hipMemsetAsync(d_blob, 0, words * 4, c->stream));
+        hipLaunchKernelGGL(occx_mask_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                           c->d_cells, r[0], r[1], r[2], c->occ_nb[0], c->occ_nb[1], (uint32_t)nb, d_masks, d_blob);
+        hipLaunchKernelGGL(occx_pack_kernel, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)d_blob,
+                           (uint32_t)nbw, (const unsigned long long*)d_masks,
+                           reinterpret_cast<uint16_t*>(d_blob + nbw),
+                           reinterpret_cast<unsigned long long*>(d_blob + moff), d_n);
+        const hipError_t le = hipGetLastError();
+        HIP_TRY(hipMemcpyAsync(c->d_occ, d_blob, nbw * 4, hipMemcpyDeviceToDevice, c->stream));
+        uint32_t run = 0;
+        HIP_TRY(hipMemcpyAsync(&run, d_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)hipFree(d_masks);
+        (void)hipFree(d_n);
+        HIP_TRY(le);
+        occx_layout(nbw, run, &moff, &words);
+        c->occx_ok = run < 0xFFFF && words * 4 <= kOccxBudget;
+        c->occx_words = (uint32_t)words;
+        c->occx_nbw = (uint32_t)nbw;
+        c->occx_moff = (uint32_t)moff;
     }
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
@@ -1530,7 +1368,6 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
             c->d_cells = dg.cells;
             c->d_pos = dg.pos;
             c->d_data = dg.data;
-            c->has_ids = false;   // ZRT_MB shape ids need the host build
             if ((rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
         }
     }
@@ -1580,16 +1417,21 @@ extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t in
     return ZRT_OK;
 }
 
-static size_t wf_budget_bytes() {
-    const char* e = getenv("ZRT_WF_BYTES");
-    if (e) { const long long v = atoll(e); if (v > 0) return (size_t)v; }
-    return (size_t)40 << 30;   // queues + bounce stack of one pass (HBM is 288 GB)
-}
-
-static size_t pass_budget_bytes() {
-    const char* e = getenv("ZRT_PASS_BYTES");
-    if (e) { const long long v = atoll(e); if (v > 0) return (size_t)v; }
-    return (size_t)8 << 30;   // 8 GiB of sample radiance per pass (HBM is 288 GB)
+// Samples per pass: the caller's cfg->samples_per_pass, else as many as fit
+// a 40 GiB budget of queues + bounce planes (HBM is 288 GB; cfg3 then runs 3
+// passes of <= 86 spp) and 60% of the free device memory.
+static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P) {
+    uint64_t s_pass;
+    if (cfg->samples_per_pass) {
+        s_pass = cfg->samples_per_pass;
+    } else {
+        size_t budget = (size_t)40 << 30;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) budget = std::min(budget, free_b / 10 * 6);
+        s_pass = std::max<uint64_t>(1, budget / (per_item * P));
+    }
+    s_pass = std::min<uint64_t>(s_pass, cfg->num_samples);
+    return std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
 }
 
 extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const zrt_render_config* cfg,
@@ -1599,10 +1441,11 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (cam->w == 0 || cam->h == 0 || (uint64_t)cam->w * cam->h > 0xFFFFFFFFull) return ZRT_ERR_INVALID_ARG;
     const uint32_t nranks = cfg->num_ranks ? cfg->num_ranks : 1;
     if (cfg->rank >= nranks) return ZRT_ERR_INVALID_ARG;
-    const bool want_stats = (cfg->flags & ZRT_FLAG_COUNT_STATS) != 0;
-    const bool want_prof = getenv("ZRT_PROFILE") != nullptr;
-    const TraceFn fn = trace_fn(cfg->max_bounce, want_stats, want_prof);
-    if (!fn) return ZRT_ERR_UNSUPPORTED;
+    // the scatter mask holds one bit per bounce slot, the queue 16 bits of depth
+    if (cfg->max_bounce > 32) return ZRT_ERR_UNSUPPORTED;
+    const bool counting = (cfg->flags & ZRT_FLAG_COUNT_STATS) != 0;
+    const TraceFn cfn = count_fn(cfg->max_bounce);
+    if (counting && !cfn) return ZRT_ERR_UNSUPPORTED;
     DeviceGuard g(c->device);
 
     // packed pixel order of this rank (cached across calls)
@@ -1626,36 +1469,21 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     const uint32_t spp = cfg->num_samples;
     const uint32_t mb = cfg->max_bounce;
-    // wavefront (default) or megakernel; the counting variant is a megakernel
-    const char* mode_env = getenv("ZRT_MODE");
-    const bool wf = !want_stats && !want_prof && !(mode_env && strcmp(mode_env, "mega") == 0);
-    // "wf" (default): one fused trace+shade kernel per bounce; "split":
-    // wf_trace_kernel (lane refill) + wf_shade_kernel per bounce
-    const bool split = wf && mode_env && strcmp(mode_env, "split") == 0;
-    // per-item bytes of a pass: megakernel = the float4 sample radiance;
-    // wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per bounce
-    // slot (+ the 16 B hit record in split mode)
-    const uint64_t per_item = wf ? (96ull + 16ull + (split ? 16ull : 0ull) + 32ull * std::max<uint32_t>(mb, 1))
-                                 : 16ull;
-    size_t budget = wf ? wf_budget_bytes() : pass_budget_bytes();
-    {
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
-            budget = std::min(budget, free_b / 10 * 6);
-    }
-    uint64_t s_pass = std::max<uint64_t>(1, budget / (per_item * P));
-    s_pass = std::min<uint64_t>(s_pass, spp);
-    s_pass = std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
+    const uint32_t nb = std::max<uint32_t>(mb, 1);
+    // per-item bytes of a pass: counting megakernel = the float4 sample
+    // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per
+    // bounce slot
+    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 32ull * nb;
+    const uint64_t s_pass = pass_samples(cfg, per_item, P);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     const uint64_t T = s_pass * P;
     int rc;
-    if (wf) {
+    if (!counting) {
         if ((rc = grow(&c->d_q0, &c->q0_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * std::max<uint32_t>(mb, 1))) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 18ull * kCtrMax * (mb + 2))) != ZRT_OK) return rc;
-        if (split && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 16ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
     }
@@ -1663,109 +1491,46 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if ((rc = grow(&c->d_rgb, &c->rgb_cap, 3ull * P)) != ZRT_OK) return rc;
     const bool want_lin = outs && outs->linear_packed;
     if (want_lin && (rc = grow(&c->d_lin, &c->lin_cap, 3ull * P)) != ZRT_OK) return rc;
-    const uint32_t launches_per_pass = wf ? std::max<uint32_t>(mb, 1) : 1;
+    const uint32_t launches_per_pass = counting ? 1 : nb;
     while (c->ev_trace.size() < 2ull * npasses * launches_per_pass) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
         c->ev_trace.push_back(e);
     }
 
+    // Kernel per launch.  ZRT_PARK (while the park kernel is measured):
+    // 1 = every launch, 2 = bounce launches only; needs OccX in LDS.
+    int park_mode = 0;
+    if (const char* e = getenv("ZRT_PARK")) park_mode = atoi(e);
+    if (!c->occx_ok || counting) park_mode = 0;
+    uint32_t test_min = 24, refill_min = 32;
+    if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    const WfFn f_first = park_mode == 1 ? (WfFn)wf_park_kernel<true> : kWfPrimary;
+    const WfFn f_next = park_mode >= 1 ? (WfFn)wf_park_kernel<false> : kWfBounce;
+    const bool park_first = park_mode == 1, park_next = park_mode >= 1;
+
     // occupancy-sized persistent grids
-    const int tblock = trace_block();
-    const char* wave_env = getenv("ZRT_WAVE");
-    const bool wave_mode = wf && !split && wave_env && atoi(wave_env) == 1;
-    const size_t lds_bytes = wave_mode ? 16ull * ((c->occ_words + 3u) / 4u) + (size_t)(tblock / 64) * sizeof(WaveLds)
-                                       : 4ull * c->occ_words;
-    auto grid_for = [&](const void* f, uint32_t* blocks) -> int {
+    const size_t lds_wf = 4ull * c->occ_words;
+    const size_t lds_park = 16ull * ((c->occx_words + 3u) / 4u) + kParkSlotsBytes;
+    auto grid_for = [&](const void* f, int threads, size_t lds, uint32_t* blocks) -> int {
         int bpc = 0;
-        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, f, tblock, lds_bytes));
-        bpc = std::max(1, std::min(bpc, 2048 / tblock));
+        HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, f, threads, lds));
+        bpc = std::max(1, std::min(bpc, 2048 / threads));
         *blocks = (uint32_t)(c->num_cus * bpc);
         return ZRT_OK;
     };
-    using WfFn = void (*)(const WfParams);
-    WfFn wf_first = nullptr, wf_next = nullptr;
-    {
-        const char* e = getenv("ZRT_WF_MINW");     // tuning sweeps only
-        const int mw = e ? atoi(e) : (split ? kSplitMinWaves : kWfMinWaves);
-#define ZRT_WF_PICK(K, MW)                                                   \
-    do {                                                                     \
-        wf_first = (WfFn)K<kTriBatch, MW, true>;                             \
-        wf_next = (WfFn)K<kTriBatch, MW, false>;                             \
-    } while (0)
-#define ZRT_WF_SWITCH(K)                                                     \
-    switch (mw) {                                                            \
-        case 4: ZRT_WF_PICK(K, 4); break;                                    \
-        case 5: ZRT_WF_PICK(K, 5); break;                                    \
-        case 6: ZRT_WF_PICK(K, 6); break;                                    \
-        case 7: ZRT_WF_PICK(K, 7); break;                                    \
-        default: ZRT_WF_PICK(K, 8); break;                                   \
+    uint32_t grid_first = 0, grid_next = 0, grid_count = 0;
+    const int thr_first = park_first ? kParkBlock : kTraceThreads;
+    const int thr_next = park_next ? kParkBlock : kTraceThreads;
+    const size_t lds_first = park_first ? lds_park : lds_wf, lds_next = park_next ? lds_park : lds_wf;
+    if (counting) {
+        if ((rc = grid_for((const void*)cfn, kTraceThreads, lds_wf, &grid_count)) != ZRT_OK) return rc;
+    } else {
+        if ((rc = grid_for((const void*)f_first, thr_first, lds_first, &grid_first)) != ZRT_OK) return rc;
+        if ((rc = grid_for((const void*)f_next, thr_next, lds_next, &grid_next)) != ZRT_OK) return rc;
     }
-        const char* mbe = c->has_ids ? getenv("ZRT_MB") : nullptr;   // needs the ids
-        const char* tbe = getenv("ZRT_TB");      // tuning sweeps only
-        const int tbv = tbe ? atoi(tbe) : kTriBatch;
-        if (!wave_mode && !split && tbv != kTriBatch && (tbv == 1 || tbv == 3 || tbv == 4)) {
-            if (tbv == 1) { wf_first = (WfFn)wf_kernel<1, 6, true>; wf_next = (WfFn)wf_kernel<1, 6, false>; }
-            if (tbv == 3) { wf_first = (WfFn)wf_kernel<3, 6, true>; wf_next = (WfFn)wf_kernel<3, 6, false>; }
-            if (tbv == 4) { wf_first = (WfFn)wf_kernel<4, 6, true>; wf_next = (WfFn)wf_kernel<4, 6, false>; }
-        } else if (wave_mode) {
-            if (mw == 5) { wf_first = (WfFn)wf_wave_kernel<5, true>; wf_next = (WfFn)wf_wave_kernel<5, false>; }
-            else if (mw == 8) { wf_first = (WfFn)wf_wave_kernel<8, true>; wf_next = (WfFn)wf_wave_kernel<8, false>; }
-            else { wf_first = (WfFn)wf_wave_kernel<6, true>; wf_next = (WfFn)wf_wave_kernel<6, false>; }
-        } else if (split) {
-            ZRT_WF_SWITCH(wf_trace_kernel)
-        } else if (mbe && atoi(mbe) == 1) {
-            if (mw == 5) { wf_first = (WfFn)wf_kernel<kTriBatch, 5, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 5, false, true>; }
-            else { wf_first = (WfFn)wf_kernel<kTriBatch, 6, true, true>; wf_next = (WfFn)wf_kernel<kTriBatch, 6, false, true>; }
-        } else {
-            ZRT_WF_SWITCH(wf_kernel)
-        }
-        // the primary launch alone at another occupancy (kWfMinWaves0 unless
-        // ZRT_WF_MINW sets both; ZRT_WF_MINW0 for tuning sweeps)
-        const char* e0 = getenv("ZRT_WF_MINW0");
-        if (!e0 && !e) e0 = kWfMinWaves0 == 7 ? "7" : "6";
-        if (e0 && !split && !wave_mode && !(mbe && atoi(mbe) == 1) && tbv == kTriBatch) {
-            switch (atoi(e0)) {
-                case 4: wf_first = (WfFn)wf_kernel<kTriBatch, 4, true>; break;
-                case 5: wf_first = (WfFn)wf_kernel<kTriBatch, 5, true>; break;
-                case 6: wf_first = (WfFn)wf_kernel<kTriBatch, 6, true>; break;
-                case 7: wf_first = (WfFn)wf_kernel<kTriBatch, 7, true>; break;
-                case 8: wf_first = (WfFn)wf_kernel<kTriBatch, 8, true>; break;
-                default: break;
-            }
-        }
-#undef ZRT_WF_SWITCH
-#undef ZRT_WF_PICK
-    }
-    uint32_t grid_blocks = 0, grid_first = 0, grid_next = 0;
-    if (wf) {
-        if ((rc = grid_for((const void*)wf_first, &grid_first)) != ZRT_OK) return rc;
-        if ((rc = grid_for((const void*)wf_next, &grid_next)) != ZRT_OK) return rc;
-    } else if ((rc = grid_for((const void*)fn, &grid_blocks)) != ZRT_OK) {
-        return rc;
-    }
-    uint32_t refill = 48;
-    // XCD-aware split of the wavefront launches (wf_kernel): ZRT_XCD=0/1/2,
-    // default 2 (cfg3 64 spp, one process: 1902 vs 1855 for 1 vs 1767 for 0)
-    uint32_t xcd_mode = 2;
-    uint32_t ctr_stride = 32;   // counter stride in u32 (ZRT_CTR=1: packed)
-    if (const char* e = getenv("ZRT_CTR")) ctr_stride = atoi(e) == 1 ? 1u : 32u;
-    if (const char* e = getenv("ZRT_XCD")) xcd_mode = (uint32_t)std::max(0, std::min(2, atoi(e)));
-    // (the counter stride is what made mode 2 pay: packed, its 8+8 region
-    // counters shared lines with the others and it ran 1091 vs 1902)
-    // ray sort between bounces (ZRT_SORT = origin-region bits per axis, 0 = off)
-    uint32_t sort_bits = 0;
-    if (const char* e = getenv("ZRT_SORT")) sort_bits = (uint32_t)std::max(0, std::min(4, atoi(e)));
-    const bool sorting = wf && sort_bits > 0 && mb > 1;
-    if (!(wf && !split && !wave_mode && !sorting)) xcd_mode = 0;   // wf_kernel only
-    const uint32_t nbins = 8u << (3 * sort_bits);
-    if (sorting) {
-        if ((rc = grow(&c->d_hist, &c->hist_cap, nbins)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_cursor, &c->cursor_cap, nbins)) != ZRT_OK) return rc;
-    }
-    if (const char* e = getenv("ZRT_REFILL")) refill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    const uint32_t shade_blocks = (uint32_t)c->num_cus * 8u;
 
     TraceParams tp;
     memset(&tp, 0, sizeof tp);
@@ -1810,68 +1575,38 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         tp.s0 = s0;
         tp.total = S * P;
         const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
-        if (wf) {
-            // counters: n[k] = live paths entering bounce k, fetch[k] = work counter of launch k
-            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 18 * kCtrMax * (mb + 2), c->stream));
-            const uint32_t kCtr = ctr_stride;
-            uint32_t* n = c->d_wfc;                       // n[k * kCtr]
-            uint32_t* fetch = c->d_wfc + kCtr * (mb + 2);  // fetch[k * kCtr]
+        if (!counting) {
+            // per launch k: 8 work counters, then 8 region counts of the
+            // paths entering launch k (written by launch k - 1)
+            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 16 * kCtr * (mb + 2), c->stream));
             WfParams W;
+            memset(&W, 0, sizeof W);
             W.t = tp;
             W.stk = c->d_stk;
             W.term = c->d_term;
-            W.hit = c->d_hit;
             W.T = (uint32_t)T;
-            W.refill = refill;
-            W.sort_bits = sort_bits;
-            const uint32_t nb = std::max<uint32_t>(mb, 1);
-            if (sorting) HIP_TRY(hipMemsetAsync(c->d_hist, 0, 4ull * nbins, c->stream));
+            W.occx = c->d_occx;
+            W.occx_words = c->occx_words;
+            W.occx_nbw = c->occx_nbw;
+            W.occx_moff = c->occx_moff;
+            W.occx_nb0 = c->occx_nb[0];
+            W.occx_nb01 = c->occx_nb[0] * c->occx_nb[1];
+            W.test_min = test_min;
+            W.refill_min = refill_min;
             for (uint32_t k = 0; k < nb; ++k) {
-                if (sorting) {             // appended to q0, sorted into q1 for the next bounce
-                    W.q_in = c->d_q1;
-                    W.q_out = c->d_q0;
-                } else {
-                    W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
-                    W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
-                }
-                const bool sort_out = sorting && k + 1 < nb;
-                W.hist = sort_out ? c->d_hist : nullptr;
-                W.n_in = n + kCtr * k;
-                W.n_out = n + kCtr * (k + 1);
-                W.fetch = fetch + kCtr * k;
-                // XCD split: per launch k, 8 work counters + 8 region counts (entering k)
-                uint32_t* x8 = c->d_wfc + 2 * kCtr * (mb + 2);
-                // 1: the primary launch only (its appends go to the one queue);
-                // 2: every launch, with region queues
-                W.xcd = (xcd_mode == 2 || (xcd_mode == 1 && k == 0)) ? 1u : 0u;
-                W.ctr = kCtr;
-                W.fetch8 = x8 + kCtr * (16 * k);
-                W.n_in8 = x8 + kCtr * (16 * k + 8);
-                W.n_out8 = xcd_mode == 2 ? x8 + kCtr * (16 * (k + 1) + 8) : nullptr;
-                if (!split || mb > 0) {
-                    HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
-                    if (k == 0)
-                        hipLaunchKernelGGL(wf_first, dim3(grid_first), dim3(tblock), lds_bytes, c->stream, W);
-                    else
-                        hipLaunchKernelGGL(wf_next, dim3(grid_next), dim3(tblock), lds_bytes, c->stream, W);
-                    HIP_TRY(hipGetLastError());
-                    HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
-                    ++launches;
-                }
-                if (split) {
-                    if (k == 0)
-                        hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
-                    else
-                        hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(shade_blocks), dim3(kBlock), 0, c->stream, W);
-                    HIP_TRY(hipGetLastError());
-                }
-                if (sort_out) {
-                    hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_hist, c->d_cursor,
-                                       nbins);
-                    hipLaunchKernelGGL(sort_scatter_kernel, dim3(shade_blocks), dim3(kBlock), 0, c->stream,
-                                       (const float4*)c->d_q0, c->d_q1, (const uint32_t*)(n + kCtr * (k + 1)), c->d_cursor);
-                    HIP_TRY(hipGetLastError());
-                }
+                W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
+                W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
+                W.fetch8 = c->d_wfc + kCtr * (16 * k);
+                W.n_in8 = c->d_wfc + kCtr * (16 * k + 8);
+                W.n_out8 = c->d_wfc + kCtr * (16 * (k + 1) + 8);
+                HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                if (k == 0)
+                    hipLaunchKernelGGL(f_first, dim3(grid_first), dim3(thr_first), lds_first, c->stream, W);
+                else
+                    hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, c->stream, W);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                ++launches;
             }
             hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
                                c->d_term, c->d_stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
@@ -1879,7 +1614,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         } else {
             HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
-            hipLaunchKernelGGL(fn, dim3(grid_blocks), dim3(tblock), lds_bytes, c->stream, tp);
+            hipLaunchKernelGGL(cfn, dim3(grid_count), dim3(kTraceThreads), lds_wf, c->stream, tp);
             HIP_TRY(hipGetLastError());
             ++launches;
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
@@ -1897,41 +1632,22 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     unsigned long long hs[32];
     HIP_TRY(hipMemcpy(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost));
-    if (getenv("ZRT_PROFILE"))
-        fprintf(stderr, "{\"zrt_profile_wave_cycles\": {\"cell_tris\": %llu, \"dda\": %llu, "
-                "\"trace\": %llu, \"shade\": %llu, \"fetch\": %llu, \"total\": %llu}}\n",
-                hs[8], hs[9], hs[10], hs[11], hs[12], hs[13]);
-    if (getenv("ZRT_CELL_STATS") && want_stats)
+    // diagnostics (debugging only): counting-build walk/test trip counts,
+    // per-launch device times
+    if (getenv("ZRT_CELL_STATS") && counting)
         fprintf(stderr, "{\"zrt_profile_cells\": {\"visited\": %llu, \"loaded\": %llu, \"non_empty\": %llu, "
-                "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu, \"trips_with_tests\": %llu, \"shared_rounds\": %llu}}\n",
+                "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu, \"trips_with_tests\": %llu, "
+                "\"shared_rounds\": %llu}}\n",
                 hs[1], hs[4], hs[5], hs[2], hs[6], hs[7], hs[14], hs[15]);
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
     const bool wf_debug = getenv("ZRT_WF_DEBUG") != nullptr;
-    for (uint32_t e = 0; e + 1 < ne; e += 2) {   // trace launches only (not shade / resolve)
+    for (uint32_t e = 0; e + 1 < ne; e += 2) {   // trace launches only (not resolve)
         float t = 0.0f;
         HIP_TRY(hipEventElapsedTime(&t, c->ev_trace[e], c->ev_trace[e + 1]));
         st.trace_kernel_ms += t;
         if (wf_debug) fprintf(stderr, "{\"zrt_launch\": %u, \"ms\": %.3f}\n", e / 2, t);
-    }
-    if (wf_debug && wf) {   // live paths entering each bounce of the last pass
-        std::vector<uint32_t> nk(mb + 2, 0);
-        std::vector<uint32_t> raw(ctr_stride * (mb + 2));
-        HIP_TRY(hipMemcpy(raw.data(), c->d_wfc, 4ull * raw.size(), hipMemcpyDeviceToHost));
-        for (uint32_t k = 0; k < mb + 2; ++k) nk[k] = raw[ctr_stride * k];
-        if (xcd_mode == 2) {   // region counts (entering bounce k): 8 per launch
-            std::vector<uint32_t> r8(ctr_stride * 16 * (mb + 2));
-            HIP_TRY(hipMemcpy(r8.data(), c->d_wfc + 2 * ctr_stride * (mb + 2), 4ull * r8.size(),
-                              hipMemcpyDeviceToHost));
-            for (uint32_t k = 1; k <= mb; ++k) {
-                nk[k] = 0;
-                for (uint32_t g = 0; g < 8; ++g) nk[k] += r8[ctr_stride * (16 * k + 8 + g)];
-            }
-        }
-        fprintf(stderr, "{\"zrt_last_pass_items\": %llu, \"live\": [", (unsigned long long)T);
-        for (uint32_t k = 1; k <= mb; ++k) fprintf(stderr, "%s%u", k > 1 ? ", " : "", nk[k]);
-        fprintf(stderr, "]}\n");
     }
     st.trace_launches = launches;
     st.segments = hs[0];
@@ -1989,6 +1705,15 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             o[0] = h ? 1.0f : 0.0f; o[1] = t; o[2] = u; o[3] = v;
             break;
         }
+        case ZRT_PROBE_TRIANGLE_FLAT: {   // wf_park_kernel's branch-free test
+            const float* a = (const float*)in + 15ull * i;
+            float* o = (float*)out + 4ull * i;
+            const v3 v0 = ld3(a), v1 = ld3(a + 3), v2 = ld3(a + 6);
+            float t = 0, u = 0, v = 0;
+            const bool h = tri_ray_flat(v0, sub(v1, v0), sub(v2, v0), ld3(a + 9), ld3(a + 12), &t, &u, &v);
+            o[0] = h ? 1.0f : 0.0f; o[1] = h ? t : 0.0f; o[2] = h ? u : 0.0f; o[3] = h ? v : 0.0f;
+            break;
+        }
         case ZRT_PROBE_BBOX: {
             const float* a = (const float*)in + 12ull * i;
             float* o = (float*)out + 2ull * i;
@@ -1999,45 +1724,43 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             break;
         }
         case ZRT_PROBE_DDA: {
-            // same arithmetic as trace_ray's setup + Iterator.next, recording cells
+            // the kernels' own DDA: dda_init (Grid.traceRay) + DDA_STEP
+            // (Iterator.next).  out: [0] steps (-1: misses the bbox, -2: the
+            // incremental linear index disagreed with linearlizeCellIdx),
+            // [1..3] first cell, then per step (cell after next(), t): the
+            // reference's it.cell / it.next() pairs (linalg.zig:583-681)
             const float* a = (const float*)in + 12ull * i;
             const uint32_t* res = (const uint32_t*)aux;
-            float* o = (float*)out + (1ull + 4ull * 64) * i;
+            float* o = (float*)out + (4ull + 4ull * 64) * i;
             Bbox bb; bb.min = ld3(a); bb.max = ld3(a + 3);
             const uint32_t r3[3] = {res[0], res[1], res[2]};
             const Grid g = grid_init(bb, r3);
-            const v3 org = ld3(a + 6), d = ld3(a + 9);
-            float t_hit;
-            if (!bbox_ray(bb, org, d, &t_hit)) { o[0] = -1.0f; break; }
-            t_hit = fmaxf(0.0f, t_hit);
-            const v3 local = sub(add(org, scale(d, t_hit)), bb.min);
-            const float lq[3] = {local.x, local.y, local.z}, dq[3] = {d.x, d.y, d.z};
-            const float csq[3] = {g.cell_size.x, g.cell_size.y, g.cell_size.z};
-            uint32_t c[3], ex[3], st[3];
-            float td[3], tn[3];
-            for (int k = 0; k < 3; ++k) {
-                const bool sg = dq[k] < 0.0f;
-                const uint32_t rm1 = r3[k] - 1u;
-                uint32_t ci = f2u(lq[k] / csq[k]);
-                ci = ci < rm1 ? ci : rm1;
-                c[k] = ci; st[k] = sg ? 0xFFFFFFFFu : 1u; ex[k] = sg ? 0u : rm1;
-                td[k] = fabsf(csq[k] / dq[k]);
-                tn[k] = t_hit + ((((float)(ci + (sg ? 0u : 1u))) * csq[k] - lq[k]) / dq[k]);
-            }
+            const float bmin[3] = {bb.min.x, bb.min.y, bb.min.z}, bmax[3] = {bb.max.x, bb.max.y, bb.max.z};
+            const float cs[3] = {g.cell_size.x, g.cell_size.y, g.cell_size.z};
+            Dda s;
+            if (!dda_init(bmin, bmax, r3, cs, ld3(a + 6), ld3(a + 9), s)) { o[0] = -1.0f; break; }
+            GridK gk;
+            gk.rm0 = r3[0] - 1u; gk.rm1 = r3[1] - 1u; gk.rm2 = r3[2] - 1u;
+            gk.str1 = r3[0]; gk.str2 = r3[0] * r3[1];
+            o[1] = (float)s.c0; o[2] = (float)s.c1; o[3] = (float)s.c2;
             int nsteps = 0;
+            bool lin_ok = true;
             while (nsteps < 64) {
-                const unsigned kk = ((unsigned)(tn[0] < tn[1]) << 2) | ((unsigned)(tn[0] < tn[2]) << 1) |
-                                    (unsigned)(tn[1] < tn[2]);
-                const unsigned ax = (0xA66u >> (2u * kk)) & 3u;
+                const uint32_t c0 = s.c0, c1 = s.c1, c2 = s.c2;
+                lin_ok = lin_ok && s.lin == (c2 * r3[1] + c1) * r3[0] + c0;
+                bool crossed;
                 float te;
-                if (c[ax] == ex[ax]) te = kInf;
-                else { te = tn[ax]; c[ax] += st[ax]; tn[ax] += td[ax]; }
-                float* e = o + 1 + 4 * nsteps;
-                e[0] = (float)c[0]; e[1] = (float)c[1]; e[2] = (float)c[2]; e[3] = te;
+                DDA_STEP(s, gk, 0u, crossed, te);
+                (void)crossed;
+                float* e = o + 4 + 4 * nsteps;
+                // at the exit cell next() returns +inf and leaves the cell
+                if (te == kInf) { e[0] = (float)c0; e[1] = (float)c1; e[2] = (float)c2; }
+                else { e[0] = (float)s.c0; e[1] = (float)s.c1; e[2] = (float)s.c2; }
+                e[3] = te;
                 ++nsteps;
                 if (te == kInf) break;
             }
-            o[0] = (float)nsteps;
+            o[0] = lin_ok ? (float)nsteps : -2.0f;
             break;
         }
         case ZRT_PROBE_TO_RGB: {
@@ -2092,9 +1815,10 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
     if (!in || !out || n == 0) return ZRT_ERR_INVALID_ARG;
     size_t in_sz = 0, out_sz = 0, aux_sz = 0;
     switch (which) {
-        case ZRT_PROBE_TRIANGLE: in_sz = 60; out_sz = 16; break;
+        case ZRT_PROBE_TRIANGLE:
+        case ZRT_PROBE_TRIANGLE_FLAT: in_sz = 60; out_sz = 16; break;
         case ZRT_PROBE_BBOX: in_sz = 48; out_sz = 8; break;
-        case ZRT_PROBE_DDA: in_sz = 48; out_sz = 4 * (1 + 4 * 64); aux_sz = 12; break;
+        case ZRT_PROBE_DDA: in_sz = 48; out_sz = 4 * (4 + 4 * 64); aux_sz = 12; break;
         case ZRT_PROBE_TO_RGB: in_sz = 12; out_sz = 12; break;
         case ZRT_PROBE_RNG_F32:
         case ZRT_PROBE_RNG_NORM: in_sz = 12; out_sz = 64; break;

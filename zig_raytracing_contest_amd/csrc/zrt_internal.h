@@ -19,6 +19,11 @@ struct DevMat { DevTex tex[3]; };   // base_color, emissive, transparency
 // host with the deterministic exp/log of zrt_math.h.
 void zig_tables(double zx[257], double zf[257]);
 
+// Host threads for "all CPUs" (config.json num_threads null, main.zig:90
+// getCpuCount): the CPUs this process may run on, capped by OMP_NUM_THREADS
+// when set (the per-GPU CPU share on shared GPU hosts).
+unsigned host_threads();
+
 // Host-side packed pixel order of one rank (zrt_tile_pixels).
 int tile_pixels(uint32_t w, uint32_t h, uint32_t tile, uint32_t rank, uint32_t nranks,
                 uint32_t* out, uint32_t* count);

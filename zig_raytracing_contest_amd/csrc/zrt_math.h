@@ -308,6 +308,27 @@ ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv
     return true;
 }
 
+// tri_ray without early returns, for lanes that test different triangles
+// side by side (wf_park_kernel's test rounds): every quantity is evaluated by
+// the same f32 operations in the same order and the rejections are combined
+// at the end, so for an accepted hit t, u and v are tri_ray's bit for bit, and
+// the hit/miss answer is tri_ray's for every input (a NaN passes a rejection
+// here exactly when tri_ray's `<` / `>` against it lets it continue).
+ZHD bool tri_ray_flat(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
+    const v3 pvec = cross(d, e2);
+    const float det = dot(e1, pvec);
+    const float inv_det = 1.0f / det;
+    const v3 tvec = sub(o, v0);
+    const float u = dot(tvec, pvec) * inv_det;
+    const v3 qvec = cross(tvec, e1);
+    const float v = dot(d, qvec) * inv_det;
+    *t = dot(e2, qvec) * inv_det;
+    *uu = u;
+    *vv = v;
+    const bool rej = (det < 0.00000001f) | (u < 0.0f) | (u > 1.0f) | (v < 0.0f) | (u + v > 1.0f);
+    return !rej;
+}
+
 // ---- textures (stage3.zig:94-121) -----------------------------------------
 ZHD float tex_frac(float v) { return fabsf(v - truncf(v)); }
 ZHD int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }

@@ -49,3 +49,15 @@ def gather_image(packed, w: int, h: int, rank: int, world: int, dist, tile: int 
     for r, idx in enumerate(_indices(w, h, world, tile, packed.device)):
         img.index_copy_(0, idx, gl[r][: idx.numel() * 3].view(-1, 3))
     return img.view(h, w, 3)
+
+
+def render_gathered(context, cam, spp: int, max_bounce: int, rank: int, world: int, dist, dev_buf,
+                    stats: bool = False, tile: int = 64):
+    """One frame of bench.py's multi-GPU step: this rank's tiles rendered
+    straight into `dev_buf` (a device tensor of max_packed(...)*3 bytes,
+    zrt_outputs.device_rgb_packed: no host copy), then gather_image to rank 0.
+    Returns (assembled (h, w, 3) tensor on rank 0 / None elsewhere, render
+    result dict)."""
+    res = context.render(cam, spp, max_bounce, rank=rank, num_ranks=world, tile=tile, stats=stats,
+                         device_ptr=dev_buf.data_ptr())
+    return gather_image(dev_buf, cam.w, cam.h, rank, world, dist, tile), res

@@ -22,6 +22,8 @@ FLAG_COUNT_STATS = 0x1
 
 PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
+PROBE_TRIANGLE_FLAT = 8
+DDA_PROBE_WIDTH = 4 + 4 * 64      # floats per ray: steps, first cell, 64 x (cell, t)
 
 
 class ZrtError(RuntimeError):
@@ -67,7 +69,8 @@ class Camera(C.Structure):
 class RenderConfig(C.Structure):
     _fields_ = [("num_samples", C.c_uint32), ("max_bounce", C.c_uint32), ("seed", C.c_uint64),
                 ("device", C.c_int32), ("rank", C.c_uint32), ("num_ranks", C.c_uint32),
-                ("tile_size", C.c_uint32), ("flags", C.c_uint32), ("_reserved", C.c_uint32 * 5)]
+                ("tile_size", C.c_uint32), ("flags", C.c_uint32), ("samples_per_pass", C.c_uint32),
+                ("_reserved", C.c_uint32 * 4)]
 
 
 class Stats(C.Structure):
@@ -91,7 +94,7 @@ EXPORTS = [
     "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
     "zrt_context_create", "zrt_context_create_built", "zrt_context_grid_info", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
     "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
-    "zrt_camera_from_matrix", "zrt_probe",
+    "zrt_camera_from_matrix", "zrt_probe", "zrt_timed_kernels",
 ]
 
 
@@ -132,6 +135,8 @@ def lib():
     L.zrt_camera_from_matrix.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int32,
                                          C.c_int32, C.POINTER(Camera)]
     L.zrt_probe.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+    L.zrt_timed_kernels.restype = C.c_char_p
+    L.zrt_timed_kernels.argtypes = []
     if hasattr(L, "zrt_gltf_load"):
         L.zrt_gltf_load.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]
         L.zrt_gltf_soup.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 4 + [
@@ -286,11 +291,12 @@ class Context:
 
     def render(self, cam: Camera, spp: int, max_bounce: int, seed: int = 0, rank: int = 0,
                num_ranks: int = 1, tile: int = 64, stats: bool = False, image=None,
-               packed=False, linear=False, device_ptr=None):
+               packed=False, linear=False, device_ptr=None, samples_per_pass=0):
         cfg = RenderConfig()
         cfg.num_samples, cfg.max_bounce, cfg.seed = spp, max_bounce, seed
         cfg.device, cfg.rank, cfg.num_ranks, cfg.tile_size = -1, rank, num_ranks, tile
         cfg.flags = FLAG_COUNT_STATS if stats else 0
+        cfg.samples_per_pass = samples_per_pass
         n = None
         out = Outputs()
         res = {}
@@ -311,6 +317,25 @@ class Context:
                                        C.byref(st)), "zrt_context_render")
         res["stats"] = st.as_dict()
         return res
+
+
+def render_oneshot(scene: Scene, cam: Camera, spp: int, max_bounce: int, seed: int = 0,
+                   device: int = -1):
+    """zrt_render: the one-shot drop-in for Scene.render (stage3.zig:247) --
+    upload, render the whole image, download, free.  Returns (h, w, 3) RGB8."""
+    cfg = RenderConfig()
+    cfg.num_samples, cfg.max_bounce, cfg.seed, cfg.device = spp, max_bounce, seed, device
+    cfg.num_ranks = 1
+    img = np.zeros((cam.h, cam.w, 3), np.uint8)
+    st = Stats()
+    check(lib().zrt_render(C.byref(scene), C.byref(cam), C.byref(cfg), img.ctypes.data, C.byref(st)),
+          "zrt_render")
+    return img, st.as_dict()
+
+
+def timed_kernels():
+    """Mangled-name substrings of the timed kernel instantiations (no HIP call)."""
+    return lib().zrt_timed_kernels().decode().split(",")
 
 
 def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=None, device=-1):
