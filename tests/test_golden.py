@@ -90,12 +90,12 @@ def test_gpu_reproduces_vector_goldens():
     assert np.array_equal(out[hit, 1:], v["tri_tuv"][hit])
     m = len(v["dda_box"])
     inp = np.concatenate([v["dda_box"], v["dda_o"], v["dda_d"]], 1).astype(np.float32)
-    out = native.probe(native.PROBE_DDA, inp, m, (m, 1 + 4 * 64), aux=v["dda_res"])
+    out = native.probe(native.PROBE_DDA, inp, m, (m, native.DDA_PROBE_WIDTH), aux=v["dda_res"])
     for i in range(m):
         k = int(v["dda_steps"][i])
         assert int(out[i, 0]) == k
         if k > 0:
-            got = out[i, 1:1 + 4 * k].reshape(k, 4)
+            got = out[i, 4:4 + 4 * k].reshape(k, 4)
             assert np.array_equal(got[:, :3].astype(np.uint32), v["dda_cells"][i, :k])
             assert np.array_equal(got[:, 3], v["dda_t"][i, :k])
     q = len(v["rgb_in"])

@@ -338,9 +338,18 @@ def timed_kernels():
     return lib().zrt_timed_kernels().decode().split(",")
 
 
+# bytes per item the probe reads / writes (render.hip zrt_probe)
+_PROBE_IO = {PROBE_TRIANGLE: (60, 16), PROBE_TRIANGLE_FLAT: (60, 16), PROBE_BBOX: (48, 8),
+             PROBE_DDA: (48, 4 * DDA_PROBE_WIDTH), PROBE_TO_RGB: (12, 12), PROBE_RNG_F32: (12, 64),
+             PROBE_RNG_NORM: (12, 64), PROBE_EXP_LOG: (8, 16), PROBE_TEXTURE: (8, 12)}
+
+
 def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=None, device=-1):
     inp = np.ascontiguousarray(inp)
     out = np.zeros(out_shape, out_dtype)
+    in_b, out_b = _PROBE_IO[which]
+    if inp.nbytes < n * in_b or out.nbytes < n * out_b:
+        raise ValueError(f"probe {which}: buffers too small for {n} items")
     auxp = None if aux is None else np.ascontiguousarray(aux).ctypes.data
     check(lib().zrt_probe(which, inp.ctypes.data, out.ctypes.data, n, auxp, device), "zrt_probe")
     return out
