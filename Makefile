@@ -18,8 +18,9 @@ LIB       := $(PKG)/libzrt.so
 CLI       := $(PKG)/bin/zrt
 
 PROBE     := tools/bin/dpp_probe
+SWEEP_LIB := tools/bin/sweep/libzrt.so
 
-all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) $(PROBE) oracle
+all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) $(PROBE) $(SWEEP_LIB) oracle
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) $(wildcard $(SRC)/*.h)
 	@mkdir -p $(OBJ)
@@ -43,6 +44,14 @@ $(PROBE): tools/dpp_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
+# Tuning build (tools only, never loaded by tests or bench): the park-kernel
+# schedule read from ZRT_PARK_T / ZRT_PARK_R; used through ZRT_LIB=<path>.
+sweep: $(SWEEP_LIB)
+$(SWEEP_LIB): $(SRC)/render.hip $(HDRS) $(filter-out $(OBJ)/render.o,$(HIP_OBJS)) $(HOST_OBJS)
+	@mkdir -p tools/bin/sweep
+	$(HIPCC) $(HIPFLAGS) -DZRT_SWEEP -c $(SRC)/render.hip -o tools/bin/sweep/render.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ tools/bin/sweep/render.o $(filter-out $(OBJ)/render.o,$(HIP_OBJS)) $(HOST_OBJS) -lz -pthread
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -50,4 +59,4 @@ clean:
 	rm -rf build $(LIB) $(PKG)/bin tools/bin
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle sweep

@@ -235,25 +235,20 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 
 
 # The timed kernels (no counting build) against the oracle on every scene:
-# wf_kernel (per-lane walk), the park kernel on the bounce launches or on
-# every launch, and the park schedule at its extremes (a test round as soon
-# as one lane parks / only when all 64 have; refill per lane / per wave).
-MODES = [("wf", {}), ("park-bounces", {"ZRT_PARK": "2"}), ("park-all", {"ZRT_PARK": "1"}),
-         ("park-eager", {"ZRT_PARK": "1", "ZRT_PARK_T": "1", "ZRT_PARK_R": "1"}),
-         ("park-lazy", {"ZRT_PARK": "1", "ZRT_PARK_T": "64", "ZRT_PARK_R": "64"})]
+# the default (wf_kernel primary launch, park kernel bounces), per-lane
+# walks everywhere (the fallback when OccX does not fit), the park kernel on
+# every launch.
+MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("park-all", native.FLAG_PARK_PRIMARY)]
 
 
-@pytest.mark.parametrize("mode,env", MODES, ids=[m for m, _ in MODES])
+@pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])
 @pytest.mark.parametrize("name,camname,w,h,spp", CASES)
-def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mode, env, name, camname,
-                                         w, h, spp):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, mode, flags, name, camname, w, h, spp):
     soup = scenes.get_scene(name)
     c = soup.camera(camname)
     aspect = c.aspect
     cam = camera_for(soup, camname, None if aspect else w, h)
-    img, res = gpu_scenes(name).render(cam, num_samples=spp, max_bounce=4, linear=True)
+    img, res = gpu_scenes(name).render(cam, num_samples=spp, max_bounce=4, linear=True, flags=flags)
     ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, aspect, None if aspect else w, h)
     rgb, lin, ctr = oracle_mod.OracleScene(soup).render(ocam, spp, 4, oracle_mod.RNG_PATH, 0, 16)
     pix = native.tile_pixels(cam.w, cam.h)
@@ -262,35 +257,31 @@ def test_render_modes_bitexact_vs_oracle(oracle_mod, gpu_scenes, monkeypatch, mo
     assert res["stats"]["segments"] == int(ctr[0])
 
 
-@pytest.mark.parametrize("mode,env", MODES[:3], ids=[m for m, _ in MODES[:3]])
-def test_render_multipass_and_ranks_identical(gpu_scenes, monkeypatch, mode, env):
+@pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])
+def test_render_multipass_and_ranks_identical(gpu_scenes, mode, flags):
     """Pass splits (sample ranges), rank splits (tile sets), the timed kernels
     and the counting megakernel all give the same image."""
     soup = scenes.get_scene("cornell")
     cam = camera_for(soup, None, 96, 80)
     rs = gpu_scenes("cornell")
     ref, _ = rs.render(cam, num_samples=6, max_bounce=4, stats=True)     # counting build
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    multi, r2 = rs.render(cam, num_samples=6, max_bounce=4, samples_per_pass=2)
+    multi, r2 = rs.render(cam, num_samples=6, max_bounce=4, samples_per_pass=2, flags=flags)
     assert r2["stats"]["trace_launches"] == 3 * 4
     assert np.array_equal(ref, multi)
     img = np.zeros_like(ref)
     for r in range(3):
-        rs.render(cam, img=img, num_samples=6, max_bounce=4, rank=r, num_ranks=3)
+        rs.render(cam, img=img, num_samples=6, max_bounce=4, rank=r, num_ranks=3, flags=flags)
     assert np.array_equal(ref, img)
 
 
-@pytest.mark.parametrize("mode,env", MODES[:3] + [("counting", {})], ids=[m for m, _ in MODES[:3]] + ["counting"])
+@pytest.mark.parametrize("mode,flags", MODES + [("counting", 0)], ids=[m for m, _ in MODES] + ["counting"])
 @pytest.mark.parametrize("mb", [0, 1, 5, 9, 17, 32])
-def test_render_max_bounce_variants(oracle_mod, gpu_scenes, monkeypatch, mode, env, mb):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def test_render_max_bounce_variants(oracle_mod, gpu_scenes, mode, flags, mb):
     soup = scenes.get_scene("cornell")
     c = soup.camera()
     cam = camera_for(soup, None, 40, 40)
     img, res = gpu_scenes("cornell").render(cam, num_samples=2, max_bounce=mb, linear=True,
-                                            stats=mode == "counting")
+                                            stats=mode == "counting", flags=flags)
     ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, 40, 40)
     rgb, lin, _ = oracle_mod.OracleScene(soup).render(ocam, 2, mb, oracle_mod.RNG_PATH, 0, 16)
     assert np.array_equal(img.reshape(-1, 3), rgb)
@@ -312,3 +303,44 @@ def test_render_rejects_bad_config(gpu_scenes):
     with pytest.raises(native.ZrtError) as e:
         gpu_scenes("sphere").render(cam, num_samples=1, max_bounce=33)
     assert e.value.status == -5
+
+
+_SCHEDULE_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+sys.path[:0] = [os.environ["ZRT_ROOT"], os.path.join(os.environ["ZRT_ROOT"], "oracle")]
+from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
+import oracle as orc
+out = {}
+for name, cam_name, h, spp in (("contest", "Camera 1", 54, 2), ("sponza", None, 40, 2), ("sphere", None, 40, 3)):
+    soup = scenes.get_scene(name)
+    c = soup.camera(cam_name)
+    cam = camera_for(soup, cam_name, None if c.aspect else h, h)
+    rs = RenderScene(soup, device=0)
+    img, _ = rs.render(cam, num_samples=spp, max_bounce=4, flags=native.FLAG_PARK_PRIMARY)
+    rs.close()
+    ocam = orc.camera_from_matrix(c.matrix, c.yfov, c.aspect, None if c.aspect else h, h)
+    rgb, _, _ = orc.OracleScene(soup).render(ocam, spp, 4, orc.RNG_PATH, 0, 16)
+    out[name] = bool(np.array_equal(img.reshape(-1, 3), rgb))
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("t,r", [(1, 1), (64, 64), (1, 64), (64, 1), (5, 37)])
+def test_park_schedule_extremes_bitexact(t, r):
+    """The park kernel's wave schedule at its extremes -- a test round as soon
+    as one lane parks or only once all 64 have; shade + refill per lane or per
+    wave -- must not change a bit (ZRT_SWEEP build, tools/bin/sweep)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "tools", "bin", "sweep", "libzrt.so")
+    if not os.path.exists(lib):
+        pytest.fail("tools/bin/sweep/libzrt.so not built (make)")
+    env = dict(os.environ, ZRT_LIB=lib, ZRT_ROOT=root, ZRT_PARK_T=str(t), ZRT_PARK_R=str(r))
+    p = subprocess.run([sys.executable, "-c", _SCHEDULE_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert all(res.values()), res

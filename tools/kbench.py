@@ -36,15 +36,16 @@ if a.cell_stats:
     ctx.close()
 for var in (a.var or [""]):
     env = dict(kv.split("=") for kv in var.split(",") if kv)
+    flags = int(env.pop("FLAGS", "0"), 0)   # zrt_render_config.flags (ZRT_FLAG_*)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     ctx = native.Context(geo.scene)
     img = np.zeros((cam.h, cam.w, 3), np.uint8)
-    ctx.render(cam, a.spp, cfg["max_bounce"], image=img)   # warm
+    ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags)   # warm
     ts = []
     for _ in range(a.reps):
         t0 = time.perf_counter()
-        r = ctx.render(cam, a.spp, cfg["max_bounce"], image=img)
+        r = ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags)
         ts.append(time.perf_counter() - t0)
     st = r["stats"]
     same = True if ref is None else bool(np.array_equal(ref, img))

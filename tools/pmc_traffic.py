@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of the dominant kernel from rocprofv3 --pmc passes.
 
-  python tools/pmc_traffic.py gpurun_out/<tag> [--kernel wf_kernel] [--out profiles/x.json]
+  python tools/pmc_traffic.py gpurun_out/<tag> [--kernel REGEX] [--out profiles/x.json]
 
 Reads <dir>/pmc_FETCH_SIZE/*counter_collection.csv and <dir>/pmc_WRITE_SIZE/...
 (one counter per pass, as MI355X_MICROARCH.md's TCC budget requires), sums
@@ -15,6 +15,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 
 def per_dispatch(path, kernel):
@@ -23,7 +24,7 @@ def per_dispatch(path, kernel):
         raise SystemExit(f"no counter_collection.csv under {path}")
     agg = collections.OrderedDict()
     for r in csv.DictReader(open(files[0])):
-        if kernel in r["Kernel_Name"]:
+        if re.search(kernel, r["Kernel_Name"]):
             k = int(r["Dispatch_Id"])
             agg[k] = agg.get(k, 0.0) + float(r["Counter_Value"])
     return agg
@@ -32,7 +33,8 @@ def per_dispatch(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="wf_kernel")
+    ap.add_argument("--kernel", default=r"wf_kernel|wf_park_kernel",
+                    help="regex over the demangled kernel names: the trace launches")
     ap.add_argument("--out")
     ap.add_argument("--workload", default="")
     a = ap.parse_args()

@@ -92,7 +92,7 @@ class RenderScene:
     def render(self, camera: native.Camera, img: Optional[np.ndarray] = None, num_samples: int = 3,
                max_bounce: int = 4, seed: int = 0, rank: int = 0, num_ranks: int = 1,
                stats: bool = False, linear: bool = False, packed: bool = False,
-               samples_per_pass: int = 0):
+               samples_per_pass: int = 0, flags: int = 0):
         """Fills img (h, w, 3) uint8 (this rank's pixels) and returns (img, extras)."""
         if img is None:
             img = np.zeros((camera.h, camera.w, 3), np.uint8)
@@ -100,5 +100,5 @@ class RenderScene:
             img.flags["C_CONTIGUOUS"]
         res = self.context.render(camera, num_samples, max_bounce, seed=seed, rank=rank,
                                   num_ranks=num_ranks, stats=stats, image=img, linear=linear,
-                                  packed=packed, samples_per_pass=samples_per_pass)
+                                  packed=packed, samples_per_pass=samples_per_pass, flags=flags)
         return img, res

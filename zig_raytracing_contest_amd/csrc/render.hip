@@ -580,7 +580,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 
 // ---------------------------------------------------------------------------
 // wf_park_kernel: Scene.traceRay as walk / park / test rounds with exact
-// per-cell occupancy in LDS (opt-in, ZRT_PARK=1, while it is measured).
+// per-cell occupancy in LDS: the bounce launches' kernel.
 //
 // Counted on the contest stand-in (cfg3, round 1): a segment visits 85
 // cells, 4.3 of them non-empty, and tests 18.2 triangles; per wave the
@@ -908,6 +908,13 @@ using WfFn = void (*)(const WfParams);
 // exactly these two (tests/test_codegen.py reads them from zrt_timed_kernels).
 constexpr int kWfMinWaves = 6;
 constexpr int kWfMinWaves0 = 6;
+// wf_park_kernel schedule: a test round once 12 lanes are parked, a shade +
+// refill round once 16 lanes are finished (cfg3 64 spp sweep, r02d: T 4-16 x
+// R 8/16/32; T 12 R 16 3110 Mrays/s, T 8-16 R 16 within 1.3%, R 8 -15%,
+// R 32 -13%; cfg5 T 16 R 16 2075, T 8 2055).  ZRT_SWEEP builds read
+// ZRT_PARK_T / ZRT_PARK_R.
+constexpr uint32_t kParkTestMin = 12;
+constexpr uint32_t kParkRefillMin = 16;
 const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true>;
 const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false>;
 
@@ -1498,17 +1505,21 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         c->ev_trace.push_back(e);
     }
 
-    // Kernel per launch.  ZRT_PARK (while the park kernel is measured):
-    // 1 = every launch, 2 = bounce launches only; needs OccX in LDS.
-    int park_mode = 0;
-    if (const char* e = getenv("ZRT_PARK")) park_mode = atoi(e);
-    if (!c->occx_ok || counting) park_mode = 0;
-    uint32_t test_min = 24, refill_min = 32;
+    // Kernel per launch: the park kernel for the bounce launches (incoherent
+    // rays) when the scene's OccX fits the LDS budget, wf_kernel for the
+    // primary launch (coherent 8x8-pixel waves: 22 vs 42 ms at cfg3 64 spp,
+    // r02d).  ZRT_FLAG_LANE_WALK: wf_kernel for every launch (the fallback);
+    // ZRT_FLAG_PARK_PRIMARY: the park kernel for the primary launch too.
+    const bool can_park = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK);
+    const bool park_next = can_park;
+    const bool park_first = can_park && (cfg->flags & ZRT_FLAG_PARK_PRIMARY);
+    uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
+#ifdef ZRT_SWEEP
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
-    const WfFn f_first = park_mode == 1 ? (WfFn)wf_park_kernel<true> : kWfPrimary;
-    const WfFn f_next = park_mode >= 1 ? (WfFn)wf_park_kernel<false> : kWfBounce;
-    const bool park_first = park_mode == 1, park_next = park_mode >= 1;
+#endif
+    const WfFn f_first = park_first ? (WfFn)wf_park_kernel<true> : kWfPrimary;
+    const WfFn f_next = park_next ? (WfFn)wf_park_kernel<false> : kWfBounce;
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;

@@ -11,14 +11,15 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzrt.so")
+# ZRT_LIB: an alternative build of the library (tools/ tuning builds only)
+LIB_PATH = os.environ.get("ZRT_LIB") or os.path.join(_HERE, "libzrt.so")
 _lib = None
 
 ZRT_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime error",
           -4: "out of memory", -5: "unsupported configuration", -6: "I/O error",
           -7: "parse error", -8: "not found", -9: "camera/output size rules violated"}
-FLAG_COUNT_STATS = 0x1
+FLAG_COUNT_STATS, FLAG_LANE_WALK, FLAG_PARK_PRIMARY = 0x1, 0x2, 0x4
 
 PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
@@ -291,11 +292,11 @@ class Context:
 
     def render(self, cam: Camera, spp: int, max_bounce: int, seed: int = 0, rank: int = 0,
                num_ranks: int = 1, tile: int = 64, stats: bool = False, image=None,
-               packed=False, linear=False, device_ptr=None, samples_per_pass=0):
+               packed=False, linear=False, device_ptr=None, samples_per_pass=0, flags=0):
         cfg = RenderConfig()
         cfg.num_samples, cfg.max_bounce, cfg.seed = spp, max_bounce, seed
         cfg.device, cfg.rank, cfg.num_ranks, cfg.tile_size = -1, rank, num_ranks, tile
-        cfg.flags = FLAG_COUNT_STATS if stats else 0
+        cfg.flags = (FLAG_COUNT_STATS if stats else 0) | flags
         cfg.samples_per_pass = samples_per_pass
         n = None
         out = Outputs()
