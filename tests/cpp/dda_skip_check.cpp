@@ -50,15 +50,28 @@ static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
     return out;
 }
 
-// product: skip unoccupied bricks whole
+static uint64_t g_texit_fails = 0;
+
+// product: skip unoccupied bricks whole; each skip's T_EXIT must be the exit
+// t of the last cell the cell walk passes in that brick (+inf at the grid
+// exit), and its state the cell walk's state on entering the next brick
 static std::vector<Rec> walk_skip(const TestGrid& g, const GridK& k, Dda s, uint64_t* skips) {
     std::vector<Rec> out;
     for (int guard = 0; guard < 100000; ++guard) {
         const bool occ = g.occupied(s.c0, s.c1, s.c2);
         if (!occ && s.neg < 8u) {
+            Dda q = s;
+            float last = 0.0f;
+            for (;;) {
+                bool cr;
+                DDA_STEP(q, k, 2, cr, last);
+                if (cr || last == kInf) break;
+            }
             bool exited;
-            BRICK_SKIP4(s, k, exited);
+            float te;
+            BRICK_SKIP4(s, k, exited, te);
             ++*skips;
+            if (memcmp(&te, &last, 4) != 0 || (!exited && !(rec(s) == rec(q)))) ++g_texit_fails;
             if (exited) return out;
             continue;
         }
@@ -129,8 +142,9 @@ int main(int argc, char** argv) {
             }
         }
     }
-    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"fails\": %llu}\n",
+    fails += g_texit_fails;
+    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, \"fails\": %llu}\n",
            (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
-           (unsigned long long)fails);
+           (unsigned long long)g_texit_fails, (unsigned long long)fails);
     return fails ? 1 : 0;
 }

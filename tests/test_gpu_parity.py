@@ -238,7 +238,9 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 # the default (wf_kernel primary launch, park kernel bounces), per-lane
 # walks everywhere (the fallback when OccX does not fit), the park kernel on
 # every launch.
-MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("park-all", native.FLAG_PARK_PRIMARY)]
+MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("park-all", native.FLAG_PARK_PRIMARY),
+         ("park-inline", native.FLAG_PARK_INLINE),
+         ("park-all-inline", native.FLAG_PARK_PRIMARY | native.FLAG_PARK_INLINE)]
 
 
 @pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])

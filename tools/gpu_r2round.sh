@@ -26,6 +26,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   [ $rc -eq 0 ] || exit $rc
 done
 i=0
+mkdir -p $out/sq
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \
            "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS TCC_HIT_sum TCC_MISS_sum" \
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do

@@ -103,10 +103,13 @@ struct GridK {
 // merge of the three sequences ordered by (t, -axis).  The brick is left by
 // the first, in that order, of the brick-exit crossings E_a = T_a(m_a)
 // (m_a = cells to the brick face along a), and every other axis b has then
-// taken exactly the crossings T_b(j), j < m_b, that precede it.  Only used
-// while nothing is hit yet (nearest = inf: no cell of an empty brick can end
-// the walk except the grid exit) and with no -inf/NaN sequence (neg bit 3).
-// EXITED: the skip left the grid (traceRay returns no hit).
+// taken exactly the crossings T_b(j), j < m_b, that precede it.  Not used
+// with a -inf/NaN sequence (neg bit 3).  EXITED: the skip left the grid
+// (Iterator.next returned +inf there).  T_EXIT: the exit t of the last cell
+// passed = the largest of the passed cells' exit ts (the merge is
+// nondecreasing), +inf if EXITED: traceRay's break test (stage3.zig:179-182)
+// fires inside the skipped cells iff nearest <= T_EXIT, and they hold no
+// triangle, so the skip is exact for any nearest.
 #define SKIP_AXIS(S, G, A)                                                                    \
     const bool n##A##_ = ((S).neg >> A) & 1u;                                                 \
     const uint32_t lo##A##_ = (S).c##A & ~3u;                                                 \
@@ -129,7 +132,7 @@ struct GridK {
               : (k##A##_ == 1u ? T##A##2_                                                     \
               : (k##A##_ == 2u ? T##A##3_ : (k##A##_ == 3u ? T##A##4_ : T##A##4_ + (S).td##A))); \
     (S).c##A = n##A##_ ? (S).c##A - k##A##_ : (S).c##A + k##A##_;
-#define BRICK_SKIP4(S, G, EXITED)                                                             \
+#define BRICK_SKIP4(S, G, EXITED, T_EXIT)                                                     \
     do {                                                                                      \
         SKIP_AXIS(S, G, 0)                                                                    \
         SKIP_AXIS(S, G, 1)                                                                    \
@@ -142,6 +145,7 @@ struct GridK {
         SKIP_COUNT(S, 1, x0_)                                                                 \
         SKIP_COUNT(S, 2, !x2_)                                                                \
         (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                       \
+        (T_EXIT) = (EXITED) ? kInf : ex_;                                                     \
         (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
     } while (0)
 

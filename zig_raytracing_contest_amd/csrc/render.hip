@@ -379,6 +379,8 @@ struct WfParams {
     uint32_t* fetch8;         // work counter per group of this launch
     const uint32_t* n_in8;    // paths per region of q_in
     uint32_t* n_out8;         // paths per region of q_out
+    float4* hit;              // split launches: [entry] (t, u, v, ref) of the segment just traced
+    uint32_t* fetch8s;        // split launches: work counter per group of the shade kernel
     // wf_park_kernel: exact per-cell occupancy blob (see OccX) and schedule
     const uint32_t* occx;
     uint32_t occx_words, occx_nbw, occx_moff, occx_nb0, occx_nb01;
@@ -657,13 +659,28 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
     return s - x;
 }
 
-template <bool PRIMARY>
+// ZRT_SWEEP builds only: per-wave s_memtime cycles of the three rounds and
+// their activity (printed by zrt_context_render as zrt_park_profile; the
+// stamps cost ~10% and never run in the product build).
+#ifdef ZRT_SWEEP
+#define PARK_PROF_DECL unsigned long long pprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    uint64_t ptick = __builtin_amdgcn_s_memtime();
+#define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
+#define PARK_COUNT(k, v) (pprof[k] += (v))
+#else
+#define PARK_PROF_DECL
+#define PARK_STAMP(k) do { } while (0)
+#define PARK_COUNT(k, v) do { } while (0)
+#endif
+
+template <bool PRIMARY, bool SPLIT>
 __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ double s_zig[514];
     for (uint32_t i = threadIdx.x; i < w.occx_words; i += blockDim.x) s_dyn[i] = w.occx[i];
-    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    if (!SPLIT)
+        for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     __syncthreads();
     OccX L;
     L.bits = s_dyn;
@@ -692,12 +709,24 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     // the path: entry index (primary item / queue index) and its region
     uint32_t qi = 0, reg = 0;
     uint32_t n_seg = 0;
+    PARK_PROF_DECL
 
     for (;;) {
         // ---- shade + refill round, once enough lanes are finished or idle
         const uint64_t busy = __ballot(st == kWalk || st == kPark);
         if ((uint32_t)(64 - __popcll(busy)) >= refill_min || busy == 0ull) {
-            if (__ballot(st == kDone) != 0ull) {
+            PARK_COUNT(8, 1);
+            PARK_COUNT(9, __popcll(__ballot(st == kDone)));
+            if (SPLIT && __ballot(st == kDone) != 0ull) {
+                // the hit record for wf_shade_kernel; then drain the stores
+                // (see below)
+                if (st == kDone) {
+                    w.hit[qi] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
+                    st = kIdle;
+                }
+                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
+            }
+            if (!SPLIT && __ballot(st == kDone) != 0ull) {
                 bool cont = false;
                 uint32_t item = 0, depth = 0, slot = 0, mask = 0;
                 Rng rng;
@@ -711,6 +740,12 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     st = kIdle;
                 }
                 wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, reg);
+                // drain the stores here: otherwise the compiler guards the
+                // walk loop's reuse of their data registers with a vmcnt(0)
+                // INSIDE the loop, which then also waits for the previous
+                // step's range load, every step (r02f ISA; walk 1304 cycles
+                // per step)
+                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
             const uint64_t idle = __ballot(st == kIdle);
             if (more && idle != 0ull) {
@@ -732,8 +767,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             d = mk(qb.x, qb.y, qb.z);
                             depth = __float_as_uint(qb.w) & 0xFFFFu;
                         }
-                        if (depth == 0u) {                         // max_bounce 0: black, nothing traced
-                            w.term[qi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        if (PRIMARY && depth == 0u) {              // max_bounce 0: black, nothing traced
+                            if (!SPLIT) w.term[qi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                         } else {
                             nearest = kInf;
                             hu = hv = 0.0f;
@@ -757,6 +792,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     }
                 }
             }
+            PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
                 if (!more) break;
                 continue;
@@ -766,6 +802,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         for (;;) {
             const uint64_t wk = __ballot(st == kWalk);
             if (wk == 0ull || (uint32_t)__popcll(__ballot(st == kPark)) >= test_min) break;
+            PARK_COUNT(3, 1);
+            PARK_COUNT(4, __popcll(wk));
             if (st == kWalk) {
                 bool crossed;
                 float t_exit;
@@ -783,11 +821,15 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
             }
         }
+        PARK_STAMP(1);
         // ---- test round: the parked lanes' cells, all pairs over all lanes
         if (__ballot(st == kPark) != 0ull) {
             const uint32_t n = st == kPark ? re - rb : 0u;
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
+            PARK_COUNT(5, 1);
+            PARK_COUNT(6, (tot + 63u) / 64u);
+            PARK_COUNT(7, tot);
             W.o[lane].w = nearest;
             W.d[lane].w = __uint_as_float(rb - off);
             W.best[lane] = ~0ull;
@@ -832,6 +874,69 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             }
             if (st == kPark) st = kWalk;                           // the cell is done: step out of it next
         }
+        PARK_STAMP(2);
+    }
+    const unsigned long long s0 = wave_sum(n_seg);
+    if (lane == 0) atomicAdd(&p.stats[0], s0);
+#ifdef ZRT_SWEEP
+    if (lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
+#endif
+}
+
+// Split launches: the shading half of a bounce (traceRayRecursive's body
+// after traceRay, stage3.zig:195-219) over the hit records wf_park_kernel
+// wrote, one lane per path with every lane of the wave busy, appending the
+// continuing paths to the next queue.  Same XCD group order as the trace.
+template <bool PRIMARY>
+__global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
+    const TraceParams& p = w.t;
+    __shared__ double s_zig[514];
+    for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    __syncthreads();
+    const double* zx = s_zig;
+    const double* zf = s_zig + 257;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    uint32_t n_seg = 0;
+    uint32_t grp = blockIdx.x & 7u, tried = 0;
+    WfParams ws = w;
+    ws.fetch8 = w.fetch8s;
+    for (;;) {
+        uint32_t base = 0, lim = 0;
+        if (!wf_fetch<PRIMARY>(ws, 64u, grp, tried, base, lim)) break;
+        const uint32_t j = base + lane;
+        bool cont = false;
+        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        Rng rng;
+        rng.s = 0;
+        if (j < lim) {
+            const uint32_t i = ent_index<PRIMARY>(p, grp, j);
+            if (PRIMARY) {
+                camera_ray(p, i, rng, o, d);
+                item = i;
+                depth = p.max_bounce;
+            } else {
+                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+                o = mk(a.x, a.y, a.z);
+                item = __float_as_uint(a.w);
+                d = mk(b.x, b.y, b.z);
+                depth = __float_as_uint(b.w) & 0xFFFFu;
+                slot = __float_as_uint(b.w) >> 16;
+                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+                mask = __float_as_uint(c.z);
+            }
+            v3 L = mk(0, 0, 0);
+            if (depth != 0) {                  // max_bounce 0: black, nothing traced
+                ++n_seg;
+                const float4 h = w.hit[i];
+                cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot,
+                                     rng, mask, L);
+            }
+            if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
+        }
+        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -983,6 +1088,7 @@ struct zrt_context {
     float4* d_term = nullptr; size_t term_cap = 0;
     float4* d_stk = nullptr; size_t stk_cap = 0;
     uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
+    float4* d_hit = nullptr; size_t hit_cap = 0;     // split park launches: hit records
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
     float* d_lin = nullptr; size_t lin_cap = 0;
@@ -1072,7 +1178,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     DeviceGuard g(c->device);
     void* bufs[] = {c->d_cells, c->d_pos,  c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ,
                     c->d_occx,  c->d_pix,  c->d_out,  c->d_q0,   c->d_q1,     c->d_term, c->d_stk,
-                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats};
+                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats, c->d_hit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -1480,7 +1586,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // per-item bytes of a pass: counting megakernel = the float4 sample
     // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per
     // bounce slot
-    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 32ull * nb;
+    // (+ the 16 B hit record of the split park launches)
+    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
     const uint64_t s_pass = pass_samples(cfg, per_item, P);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     const uint64_t T = s_pass * P;
@@ -1490,7 +1597,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * nb)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 16ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
     }
@@ -1518,8 +1625,17 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
-    const WfFn f_first = park_first ? (WfFn)wf_park_kernel<true> : kWfPrimary;
-    const WfFn f_next = park_next ? (WfFn)wf_park_kernel<false> : kWfBounce;
+    // split: the park kernel traces only (hit records), wf_shade_kernel
+    // shades with whole waves; ZRT_FLAG_PARK_INLINE: the park kernel shades
+    // in its refill rounds
+    const bool split = !(cfg->flags & ZRT_FLAG_PARK_INLINE);
+    const WfFn f_first = park_first ? (split ? (WfFn)wf_park_kernel<true, true> : (WfFn)wf_park_kernel<true, false>)
+                                    : kWfPrimary;
+    const WfFn f_next = park_next ? (split ? (WfFn)wf_park_kernel<false, true> : (WfFn)wf_park_kernel<false, false>)
+                                  : kWfBounce;
+    const WfFn s_first = (WfFn)wf_shade_kernel<true>, s_next = (WfFn)wf_shade_kernel<false>;
+    const bool shade_first = park_first && split, shade_next = park_next && split;
+    if ((shade_first || shade_next) && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
@@ -1532,7 +1648,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         *blocks = (uint32_t)(c->num_cus * bpc);
         return ZRT_OK;
     };
-    uint32_t grid_first = 0, grid_next = 0, grid_count = 0;
+    uint32_t grid_first = 0, grid_next = 0, grid_count = 0, grid_shade = 0;
     const int thr_first = park_first ? kParkBlock : kTraceThreads;
     const int thr_next = park_next ? kParkBlock : kTraceThreads;
     const size_t lds_first = park_first ? lds_park : lds_wf, lds_next = park_next ? lds_park : lds_wf;
@@ -1541,6 +1657,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     } else {
         if ((rc = grid_for((const void*)f_first, thr_first, lds_first, &grid_first)) != ZRT_OK) return rc;
         if ((rc = grid_for((const void*)f_next, thr_next, lds_next, &grid_next)) != ZRT_OK) return rc;
+        if ((rc = grid_for((const void*)s_next, kTraceThreads, 0, &grid_shade)) != ZRT_OK) return rc;
     }
 
     TraceParams tp;
@@ -1589,7 +1706,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if (!counting) {
             // per launch k: 8 work counters, then 8 region counts of the
             // paths entering launch k (written by launch k - 1)
-            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 16 * kCtr * (mb + 2), c->stream));
+            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 24 * kCtr * (mb + 2), c->stream));
             WfParams W;
             memset(&W, 0, sizeof W);
             W.t = tp;
@@ -1610,12 +1727,18 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.fetch8 = c->d_wfc + kCtr * (16 * k);
                 W.n_in8 = c->d_wfc + kCtr * (16 * k + 8);
                 W.n_out8 = c->d_wfc + kCtr * (16 * (k + 1) + 8);
+                W.hit = c->d_hit;
+                W.fetch8s = c->d_wfc + kCtr * (16 * (mb + 2) + 8 * k);
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
                 if (k == 0)
                     hipLaunchKernelGGL(f_first, dim3(grid_first), dim3(thr_first), lds_first, c->stream, W);
                 else
                     hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, c->stream, W);
                 HIP_TRY(hipGetLastError());
+                if (k == 0 ? shade_first : shade_next) {     // same bounce, shading half
+                    hipLaunchKernelGGL(k == 0 ? s_first : s_next, dim3(grid_shade), dim3(kTraceThreads), 0, c->stream, W);
+                    HIP_TRY(hipGetLastError());
+                }
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
                 ++launches;
             }
@@ -1650,6 +1773,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 "\"tests\": %llu, \"wave_cell_trips\": %llu, \"wave_tri_trips\": %llu, \"trips_with_tests\": %llu, "
                 "\"shared_rounds\": %llu}}\n",
                 hs[1], hs[4], hs[5], hs[2], hs[6], hs[7], hs[14], hs[15]);
+#ifdef ZRT_SWEEP
+    if (getenv("ZRT_PARK_PROFILE") && park_next)
+        fprintf(stderr, "{\"zrt_park_profile\": {\"cyc_shade_refill\": %llu, \"cyc_walk\": %llu, \"cyc_test\": %llu, "
+                "\"walk_iters\": %llu, \"walk_lanes\": %llu, \"test_rounds\": %llu, \"sub_rounds\": %llu, "
+                "\"pairs\": %llu, \"refill_rounds\": %llu, \"shaded_lanes\": %llu}}\n",
+                hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25]);
+#endif
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
     st.render_ms = ms;
