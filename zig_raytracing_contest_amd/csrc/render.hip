@@ -628,6 +628,20 @@ __device__ __forceinline__ uint32_t occx_bit(const Dda& s) {
     return ((s.c2 & 3u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
 }
 
+// A parked lane's cell range [begin, end) is loaded by LDS-DMA into its
+// wave's slots (begin at rng[lane], end at rng[64 + lane]): the load writes
+// no VGPR, so the walk loop that keeps stepping the other lanes never waits
+// on it (a VGPR destination made the compiler put a vmcnt(0) in the walk:
+// its address registers doubled as the previous step's load destination,
+// r02k ISA).  Nothing orders an LDS read behind a pending LDS-DMA but the
+// wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
+constexpr int kParkWaves = kParkBlock / 64;
+__device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t lin, uint32_t* rng) {
+    const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells) + 2ull * lin;
+    __builtin_amdgcn_global_load_lds(c, rng, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds(c + 1, rng + 64, 4, 0, 0);
+}
+
 // Per-wave LDS of the test rounds.
 struct ParkSlot {
     float4 o[64];                    // lane's ray origin; w: nearest entering the round
@@ -678,6 +692,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ double s_zig[514];
+    __shared__ uint32_t s_rng[kParkWaves * 128];            // LDS-DMA range slots
+    uint32_t* const rng_slot = s_rng + 128u * (threadIdx.x >> 6);
     for (uint32_t i = threadIdx.x; i < w.occx_words; i += blockDim.x) s_dyn[i] = w.occx[i];
     if (!SPLIT)
         for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
@@ -705,7 +721,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
     unsigned long long bm = 0ull;
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
-    uint32_t hidx = 0, rb = 0, re = 0;
+    uint32_t hidx = 0;
     // the path: entry index (primary item / queue index) and its region
     uint32_t qi = 0, reg = 0;
     uint32_t n_seg = 0;
@@ -778,9 +794,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s)) {   // stage3.zig:153-156
                                 bm = occx_mask(L, occx_brick(w, s));
                                 if ((bm >> occx_bit(s)) & 1ull) {
-                                    const uint2 c = p.cells[s.lin];
-                                    rb = c.x;
-                                    re = c.y;
+                                    park_load_range(p, s.lin, rng_slot);
                                     st = kPark;
                                 } else {
                                     st = kWalk;
@@ -813,9 +827,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 } else {
                     if (crossed) bm = occx_mask(L, occx_brick(w, s));
                     if ((bm >> occx_bit(s)) & 1ull) {
-                        const uint2 c = p.cells[s.lin];
-                        rb = c.x;
-                        re = c.y;
+                        park_load_range(p, s.lin, rng_slot);
                         st = kPark;
                     }
                 }
@@ -824,6 +836,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         PARK_STAMP(1);
         // ---- test round: the parked lanes' cells, all pairs over all lanes
         if (__ballot(st == kPark) != 0ull) {
+            __builtin_amdgcn_s_waitcnt(0x3f70);                    // vmcnt(0): the ranges landed
+            const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane];
             const uint32_t n = st == kPark ? re - rb : 0u;
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
@@ -1058,7 +1072,7 @@ int grow(T** p, size_t* cap, size_t n) {
 // per CU after the per-wave ParkSlots and the static ziggurat tables.
 constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
-constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - 256;
+constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 128 * 4 - 256;
 
 }  // namespace
 
@@ -1639,7 +1653,11 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
-    const size_t lds_park = 16ull * ((c->occx_words + 3u) / 4u) + kParkSlotsBytes;
+    int park_block = kParkBlock;
+#ifdef ZRT_SWEEP
+    if (const char* e = getenv("ZRT_PARK_BLOCK")) park_block = std::max(64, std::min(kParkBlock, atoi(e) / 64 * 64));
+#endif
+    const size_t lds_park = 16ull * ((c->occx_words + 3u) / 4u) + (size_t)(park_block / 64) * sizeof(ParkSlot);
     auto grid_for = [&](const void* f, int threads, size_t lds, uint32_t* blocks) -> int {
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1649,8 +1667,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         return ZRT_OK;
     };
     uint32_t grid_first = 0, grid_next = 0, grid_count = 0, grid_shade = 0;
-    const int thr_first = park_first ? kParkBlock : kTraceThreads;
-    const int thr_next = park_next ? kParkBlock : kTraceThreads;
+    const int thr_first = park_first ? park_block : kTraceThreads;
+    const int thr_next = park_next ? park_block : kTraceThreads;
     const size_t lds_first = park_first ? lds_park : lds_wf, lds_next = park_next ? lds_park : lds_wf;
     if (counting) {
         if ((rc = grid_for((const void*)cfn, kTraceThreads, lds_wf, &grid_count)) != ZRT_OK) return rc;
