@@ -21,6 +21,7 @@
 #include <array>
 #include <cmath>
 #include <memory>
+#include <new>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -258,8 +259,12 @@ int load_images(Loader& L, uint32_t nthreads, std::vector<Image8>* images) {
                 data = bytes.data();
                 len = bytes.size();
             }
-            rc[i] = (len >= 2 && data[0] == 0xFF && data[1] == 0xD8) ? jpeg_decode(data, len, &(*images)[i])
-                                                                      : png_decode(data, len, &(*images)[i]);
+            try {   // (a worker thread: nothing may escape it)
+                rc[i] = (len >= 2 && data[0] == 0xFF && data[1] == 0xD8) ? jpeg_decode(data, len, &(*images)[i])
+                                                                          : png_decode(data, len, &(*images)[i]);
+            } catch (const std::bad_alloc&) {
+                rc[i] = ZRT_ERR_OUT_OF_MEMORY;
+            }
         }
     };
     const size_t nt = std::max<size_t>(1, std::min<size_t>(nthreads ? nthreads : host_threads(), n));
@@ -274,9 +279,23 @@ int load_images(Loader& L, uint32_t nthreads, std::vector<Image8>* images) {
 
 }  // namespace
 
+static int gltf_load(const char* path, uint32_t num_threads, zrt_gltf** out);
+
+// No exception crosses the C ABI: an allocation a hostile file provokes
+// (sizes are validated against the data first) becomes an error code.
 extern "C" int zrt_gltf_load(const char* path, uint32_t num_threads, zrt_gltf** out) {
     if (!path || !out) return ZRT_ERR_INVALID_ARG;
     *out = nullptr;
+    try {
+        return gltf_load(path, num_threads, out);
+    } catch (const std::bad_alloc&) {
+        return ZRT_ERR_OUT_OF_MEMORY;
+    } catch (...) {
+        return ZRT_ERR_PARSE;
+    }
+}
+
+static int gltf_load(const char* path, uint32_t num_threads, zrt_gltf** out) {
     Loader L;
     L.dir = dirname_of(path);
     std::vector<uint8_t> file;

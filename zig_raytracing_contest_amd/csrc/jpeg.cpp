@@ -315,24 +315,27 @@ struct Decoder {
 constexpr int kCB = 13, kP1 = 2;
 constexpr int fx(double x) { return (int)(x * (1 << kCB) + 0.5); }
 
-inline void idct_1d(const int* in, int stride, int& o0, int& o1, int& o2, int& o3, int& o4, int& o5, int& o6,
-                    int& o7) {
+// 64-bit: a corrupt stream can carry coefficients whose products overflow
+// 32 bits (UB; tests/test_sanitize.py); valid data gives the same values.
+using ilong = long long;
+inline void idct_1d(const ilong* in, int stride, ilong& o0, ilong& o1, ilong& o2, ilong& o3, ilong& o4, ilong& o5,
+                    ilong& o6, ilong& o7) {
     // even part: inputs 0, 2, 4, 6
-    int z2 = in[2 * stride], z3 = in[6 * stride];
-    int z1 = (z2 + z3) * fx(0.541196100);
-    const int t2 = z1 + z3 * -fx(1.847759065);
-    const int t3 = z1 + z2 * fx(0.765366865);
+    ilong z2 = in[2 * stride], z3 = in[6 * stride];
+    ilong z1 = (z2 + z3) * fx(0.541196100);
+    const ilong t2 = z1 + z3 * -fx(1.847759065);
+    const ilong t3 = z1 + z2 * fx(0.765366865);
     z2 = in[0];
     z3 = in[4 * stride];
-    const int t0 = (z2 + z3) * (1 << kCB), t1 = (z2 - z3) * (1 << kCB);
-    const int e10 = t0 + t3, e13 = t0 - t3, e11 = t1 + t2, e12 = t1 - t2;
+    const ilong t0 = (z2 + z3) * (1 << kCB), t1 = (z2 - z3) * (1 << kCB);
+    const ilong e10 = t0 + t3, e13 = t0 - t3, e11 = t1 + t2, e12 = t1 - t2;
     // odd part: inputs 7, 5, 3, 1
-    int a0 = in[7 * stride], a1 = in[5 * stride], a2 = in[3 * stride], a3 = in[1 * stride];
+    ilong a0 = in[7 * stride], a1 = in[5 * stride], a2 = in[3 * stride], a3 = in[1 * stride];
     z1 = a0 + a3;
     z2 = a1 + a2;
     z3 = a0 + a2;
-    int z4 = a1 + a3;
-    const int z5 = (z3 + z4) * fx(1.175875602);
+    ilong z4 = a1 + a3;
+    const ilong z5 = (z3 + z4) * fx(1.175875602);
     a0 *= fx(0.298631336);
     a1 *= fx(2.053119869);
     a2 *= fx(3.072711026);
@@ -351,27 +354,30 @@ inline void idct_1d(const int* in, int stride, int& o0, int& o1, int& o2, int& o
     o3 = e13 + a0; o4 = e13 - a0;
 }
 
-inline uint8_t clamp8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+inline uint8_t clamp8(ilong v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
 void idct_block(const int16_t* coef, const uint16_t* qz, uint8_t* out, int stride) {
-    int d[64], ws[64];
-    for (int k = 0; k < 64; ++k) d[kZig[k]] = coef[kZig[k]] * (int)qz[k];
+    ilong d[64], ws[64];
+    for (int k = 0; k < 64; ++k) d[kZig[k]] = (ilong)coef[kZig[k]] * (ilong)qz[k];
     for (int c = 0; c < 8; ++c) {                 // columns
-        const int* in = d + c;
+        const ilong* in = d + c;
         if (!in[8] && !in[16] && !in[24] && !in[32] && !in[40] && !in[48] && !in[56]) {
-            const int dcv = in[0] * (1 << kP1);
+            const ilong dcv = in[0] * (1 << kP1);
             for (int r = 0; r < 8; ++r) ws[8 * r + c] = dcv;
             continue;
         }
-        int o[8];
+        ilong o[8];
         idct_1d(in, 8, o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]);
-        const int sh = kCB - kP1, rnd = 1 << (sh - 1);
-        for (int r = 0; r < 8; ++r) ws[8 * r + c] = (o[r] + rnd) >> sh;
+        const int sh = kCB - kP1;
+        const ilong rnd = 1ll << (sh - 1);
+        // (a corrupt block: keep the row pass's products inside 64 bits)
+        for (int r = 0; r < 8; ++r) ws[8 * r + c] = std::max<ilong>(-(1ll << 40), std::min<ilong>(1ll << 40, (o[r] + rnd) >> sh));
     }
     for (int r = 0; r < 8; ++r) {                 // rows: descale, +128, clamp
-        int o[8];
+        ilong o[8];
         idct_1d(ws + 8 * r, 1, o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]);
-        const int sh = kCB + kP1 + 3, rnd = (1 << (sh - 1)) + (128 << sh);
+        const int sh = kCB + kP1 + 3;
+        const ilong rnd = (1ll << (sh - 1)) + (128ll << sh);
         for (int k = 0; k < 8; ++k) out[(size_t)r * stride + k] = clamp8((o[k] + rnd) >> sh);
     }
 }
@@ -490,6 +496,7 @@ int jpeg_decode(const uint8_t* data, size_t len, Image8* out) {
             D.width = D.u16();
             D.ncomp = D.u8();
             if (D.width <= 0 || D.height <= 0) return ZRT_ERR_UNSUPPORTED;   // DNL not supported
+            if ((uint64_t)D.width * D.height > (1ull << 27)) return ZRT_ERR_UNSUPPORTED;   // > 128 MP
             if (D.ncomp != 1 && D.ncomp != 3) return ZRT_ERR_UNSUPPORTED;   // CMYK / YCCK
             for (int i = 0; i < D.ncomp; ++i) {
                 Comp& c = D.comp[i];

@@ -122,6 +122,10 @@ int png_decode(const uint8_t* d, size_t n, Image8* out) {
         const size_t ph = (h > (uint32_t)passes[k].y0) ? (h - passes[k].y0 + passes[k].dy - 1) / passes[k].dy : 0;
         if (pw && ph) total += ph * (1 + (pw * bits_pp + 7) / 8);
     }
+    // deflate expands at most ~1032:1: a header promising more than the
+    // IDAT data can hold is corrupt (and must not drive a huge allocation)
+    if ((uint64_t)w * h > (1ull << 27) || total > (size_t)1 << 31 || total > idat.size() * (size_t)1040 + 1024)
+        return ZRT_ERR_PARSE;
     std::vector<uint8_t> raw(total);
     {
         z_stream zs;

@@ -526,8 +526,12 @@ def get_scene(name: str) -> SceneSoup:
 
 
 # ------------------------------------------------------------------ glTF out
-def write_gltf(soup: SceneSoup, path: str) -> str:
+def write_gltf(soup: SceneSoup, path: str, jpeg_quality: Optional[int] = None) -> str:
     """Write `soup` as .gltf + .bin (+ .png textures) next to `path`.
+
+    jpeg_quality: write the textures without alpha as baseline JPEG (PIL) at
+    that quality instead of PNG (lossy: the loader's texels then differ from
+    `soup`'s; tests compare against the loaded scene).
 
     Identity node transforms (positions/texcoords load back bit-exact; normals
     load back as normalize(n), the reference's loader step), u16 indices as
@@ -587,8 +591,15 @@ def write_gltf(soup: SceneSoup, path: str) -> str:
     f = lambda x: float(np.float32(x))  # noqa: E731  f32-exact decimal
     images, textures, samplers = [], [], []
     for i, t in enumerate(soup.textures):
-        fn = f"{name}_tex{i}.png"
-        pngio.write(os.path.join(d, fn), t.rgba if t.has_alpha else t.rgba[..., :3])
+        opaque = bool(np.all(t.rgba[..., 3] == 255))
+        if jpeg_quality is not None and opaque:
+            from PIL import Image
+            fn = f"{name}_tex{i}.jpg"
+            Image.fromarray(np.ascontiguousarray(t.rgba[..., :3]), "RGB").save(
+                os.path.join(d, fn), "JPEG", quality=int(jpeg_quality))
+        else:
+            fn = f"{name}_tex{i}.png"
+            pngio.write(os.path.join(d, fn), t.rgba if t.has_alpha else t.rgba[..., :3])
         images.append({"uri": fn})
         samplers.append({"wrapS": 33071 if t.wrap_s_clamp else 10497,
                          "wrapT": 33071 if t.wrap_t_clamp else 10497})
