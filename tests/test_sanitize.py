@@ -129,7 +129,7 @@ def test_parsers_clean_under_asan_ubsan(tmp_path):
     work.mkdir()
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:allocator_may_return_null=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
-    r = subprocess.run([exe, str(work), os.environ.get("ZRT_FUZZ_N", "200"), *seeds], capture_output=True, text=True, timeout=600, env=env)
+    r = subprocess.run([exe, str(work), os.environ.get("ZRT_FUZZ_N", "1000"), *seeds], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(res)

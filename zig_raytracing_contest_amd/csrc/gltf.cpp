@@ -18,6 +18,8 @@
 // zgltf's TRS composition and matrix product order are not recoverable
 // offline (submodule empty): "parity unpinned" for node transforms that are
 // not identity.  Images: PNG (png.cpp) and JPEG (jpeg.cpp) decoders.
+#include <sys/stat.h>
+
 #include <array>
 #include <cmath>
 #include <memory>
@@ -55,12 +57,16 @@ struct zrt_gltf {
 namespace {
 
 bool read_file(const std::string& path, std::vector<uint8_t>* out) {
+    struct stat sb;
+    // a regular file only: a URI naming a directory opens, and its "size" is
+    // LONG_MAX on some filesystems (found by tests/test_sanitize.py)
+    if (stat(path.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode)) return false;
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) return false;
     fseek(f, 0, SEEK_END);
     const long n = ftell(f);
     fseek(f, 0, SEEK_SET);
-    if (n < 0) { fclose(f); return false; }
+    if (n < 0 || (uint64_t)n > (1ull << 34)) { fclose(f); return false; }
     out->resize((size_t)n);
     const size_t r = n ? fread(out->data(), 1, (size_t)n, f) : 0;
     fclose(f);
@@ -191,9 +197,15 @@ struct Loader {
         const std::string type = ac.string("type", "");
         a->ncomp = type == "SCALAR" ? 1 : type == "VEC2" ? 2 : type == "VEC3" ? 3 : type == "VEC4" ? 4 : 0;
         a->ctype = (int)ac.integer("componentType", 0);
-        a->count = (size_t)ac.integer("count", 0);
+        const int64_t count = ac.integer("count", 0);
         a->normalized = ac.get("normalized") && ac.get("normalized")->b;
-        const int csz = (a->ctype == 5126 || a->ctype == 5125) ? 4 : (a->ctype == 5123 || a->ctype == 5122) ? 2 : 1;
+        int csz;
+        switch (a->ctype) {
+            case 5120: case 5121: csz = 1; break;
+            case 5122: case 5123: csz = 2; break;
+            case 5125: case 5126: csz = 4; break;
+            default: return ZRT_ERR_PARSE;
+        }
         const int64_t bv = ac.integer("bufferView", -1);
         if (bv < 0 || a->ncomp == 0) return ZRT_ERR_UNSUPPORTED;
         const Value* bvs = doc.get("bufferViews");
@@ -201,11 +213,21 @@ struct Loader {
         const Value& v = (*bvs)[(size_t)bv];
         const int64_t b = v.integer("buffer", -1);
         if (b < 0 || (size_t)b >= buffers.size()) return ZRT_ERR_PARSE;
-        const size_t off = (size_t)v.integer("byteOffset", 0) + (size_t)ac.integer("byteOffset", 0);
-        const size_t stride = (size_t)v.integer("byteStride", 0);
-        a->stride = stride ? stride : (size_t)csz * a->ncomp;
-        const size_t need = a->count ? off + (a->count - 1) * a->stride + (size_t)csz * a->ncomp : off;
-        if (need > buffers[(size_t)b].size()) return ZRT_ERR_PARSE;
+        // every size from the document checked before any arithmetic on it
+        // (a hostile count/offset/stride must not wrap the bounds check)
+        const int64_t o1 = v.integer("byteOffset", 0), o2 = ac.integer("byteOffset", 0);
+        const int64_t st = v.integer("byteStride", 0);
+        const uint64_t size = buffers[(size_t)b].size(), elem = (uint64_t)csz * a->ncomp;
+        if (count < 0 || count > (1ll << 31) || o1 < 0 || o2 < 0 || st < 0 || st > 255) return ZRT_ERR_PARSE;
+        if ((uint64_t)o1 > size || (uint64_t)o2 > size - (uint64_t)o1) return ZRT_ERR_PARSE;
+        const uint64_t off = (uint64_t)o1 + (uint64_t)o2;
+        a->count = (size_t)count;
+        a->stride = st ? (size_t)st : (size_t)elem;
+        if (st && (uint64_t)st < elem) return ZRT_ERR_PARSE;
+        if (a->count) {
+            if (size - off < elem) return ZRT_ERR_PARSE;
+            if ((uint64_t)(a->count - 1) > (size - off - elem) / a->stride) return ZRT_ERR_PARSE;
+        }
         a->base = buffers[(size_t)b].data() + off;
         return ZRT_OK;
     }
@@ -380,9 +402,14 @@ static int gltf_load(const char* path, uint32_t num_threads, zrt_gltf** out) {
             if (ap.ctype != 5126 || ap.ncomp != 3) return ZRT_ERR_UNSUPPORTED;
             const bool has_n = attrs->get("NORMAL") != nullptr, has_t = attrs->get("TEXCOORD_0") != nullptr;
             if (has_n && ((rc = L.accessor(attrs->integer("NORMAL", -1), &an)) != ZRT_OK)) return rc;
+            if (has_n && (an.ctype != 5126 || an.ncomp != 3)) return ZRT_ERR_UNSUPPORTED;
             if (has_t && ((rc = L.accessor(attrs->integer("TEXCOORD_0", -1), &at)) != ZRT_OK)) return rc;
+            if (has_t && (at.ncomp != 2 || !(at.ctype == 5126 || at.ctype == 5121 || at.ctype == 5123)))
+                return ZRT_ERR_UNSUPPORTED;
             const bool indexed = pr.get("indices") != nullptr;
             if (indexed && ((rc = L.accessor(pr.integer("indices", -1), &ai)) != ZRT_OK)) return rc;
+            if (indexed && (ai.ncomp != 1 || !(ai.ctype == 5121 || ai.ctype == 5123 || ai.ctype == 5125)))
+                return ZRT_ERR_PARSE;
             const int64_t mat = pr.integer("material", -1);
             if (mat < 0) return ZRT_ERR_UNSUPPORTED;   // reference: primitive.material.? (stage1.zig:239)
             const size_t nidx = indexed ? ai.count : ap.count;

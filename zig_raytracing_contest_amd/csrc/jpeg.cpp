@@ -148,6 +148,7 @@ struct Decoder {
             h.valptr[l] = k;
             h.mincode[l] = code;
             for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
+                if (code >= (1 << l)) return false;        // over-subscribed: not a prefix code
                 if (l <= 9) {
                     const int shift = 9 - l;
                     for (int j = 0; j < (1 << shift); ++j)
