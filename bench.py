@@ -299,13 +299,15 @@ def main():
             # divergence, not by DRAM bandwidth (profiles/)
             "roofline": {"bound": "hbm", "limiter": "latency", "achieved": round(achieved, 1),
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": None, "kernel": "wf_kernel (all trace launches)",
+                         "traffic": None,
+                         "kernel": "trace launches: wf_kernel<6,true> (primary), wf_park_kernel<false,true> + "
+                                   "wf_shade_kernel<false> (each bounce)",
                          "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "alg_GB_per_launch": round(per_launch / 1e9, 3)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},
         }
-        tr = traffic_for(a.config, "wf_") if spp == cfgd["spp"] else None
+        tr = traffic_for(a.config, "wf_shade_kernel") if spp == cfgd["spp"] else None
         if tr:
             mem_gbs = tr[0] / 1e9 / avg_launch_s
             out["roofline"]["traffic"] = round(tr[0] / 1e9, 3)

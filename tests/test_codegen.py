@@ -1,6 +1,6 @@
 """Codegen guard for the timed kernels (CPU; reads the gfx950 code object).
 
-The timed wf_kernel instantiations must not touch scratch memory inside the
+The timed kernel instantiations must not touch scratch memory inside the
 cell walk: when the 7-wave bounce kernel did (2-3 spill reloads per trip), the
 bounce launches ran 9% slower with bit-identical output, which no parity test
 can see.  tools/spill_check.py does the disassembly; which
@@ -31,24 +31,36 @@ def code():
     return spill_check, spill_check.kernels(spill_check.disassemble(OBJ))
 
 
-def _walk_scratch(sc, ks, sub):
+def _kernel(ks, sub):
     names = [n for n in ks if sub in n]
     assert names, sub
-    loops = sc.walk_spills(ks[names[0]])
-    assert loops, f"no walk loop found in {names[0]}"
-    return max(s for _, _, s in loops)
+    return ks[names[0]]
 
 
 def test_timed_kernel_names_come_from_the_library():
     import spill_check
     t = spill_check.timed()
-    assert len(t) == 2 and t[0].startswith("wf_kernel") and t[1].startswith("wf_kernel")
+    assert t[0].startswith("wf_kernel") and any(n.startswith("wf_park_kernel") for n in t)
+    assert any(n.startswith("wf_shade_kernel") for n in t)
 
 
 def test_timed_kernels_do_not_spill_in_the_walk(code):
     sc, ks = code
     for sub in sc.timed():
-        assert _walk_scratch(sc, ks, sub) == 0, sub
+        ins = _kernel(ks, sub)
+        loops = sc.walk_spills(ins)
+        if sub.startswith(("wf_kernel", "wf_park_kernel")):
+            assert loops, f"no walk loop found in {sub}"
+        assert max((s for _, _, s in loops), default=0) == 0, sub
+
+
+def test_park_and_shade_kernels_use_no_scratch(code):
+    """The park and shade kernels touch no scratch at all (not only in the
+    walk): their whole state lives in VGPRs and LDS."""
+    sc, ks = code
+    for sub in sc.timed():
+        if sub.startswith(("wf_park_kernel", "wf_shade_kernel")):
+            assert not any("scratch_" in t for _, t in _kernel(ks, sub)), sub
 
 
 def test_spill_check_sees_walk_spills():

@@ -33,18 +33,21 @@ def per_dispatch(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default=r"wf_kernel|wf_park_kernel",
-                    help="regex over the demangled kernel names: the trace launches")
+    ap.add_argument("--kernel", default=r"wf_kernel|wf_park_kernel|wf_shade_kernel",
+                    help="regex over the demangled kernel names: the kernels inside the timed launches")
+    ap.add_argument("--launches", default=r"wf_kernel|wf_park_kernel",
+                    help="regex of the kernel that opens each timed launch (the per-launch divisor; a "
+                         "split park launch is wf_park_kernel + wf_shade_kernel)")
     ap.add_argument("--out")
     ap.add_argument("--workload", default="")
     a = ap.parse_args()
     f = per_dispatch(os.path.join(a.dir, "pmc_FETCH_SIZE"), a.kernel)
     w = per_dispatch(os.path.join(a.dir, "pmc_WRITE_SIZE"), a.kernel)
-    n = len(f)
-    assert n and n == len(w), (n, len(w))
+    assert f and len(f) == len(w), (len(f), len(w))
+    n = len(per_dispatch(os.path.join(a.dir, "pmc_FETCH_SIZE"), a.launches))
     fetch = 2.0 * 1024.0 * sum(f.values())      # gfx950: FETCH_SIZE is half the bytes
     write = 1024.0 * sum(w.values())
-    res = {"kernel": a.kernel, "launches": n, "fetch_bytes": fetch, "write_bytes": write,
+    res = {"kernel": a.kernel, "launches": n, "dispatches": len(f), "fetch_bytes": fetch, "write_bytes": write,
            "bytes_per_launch": (fetch + write) / n, "workload": a.workload,
            "source": os.path.basename(os.path.normpath(a.dir)),
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024"}

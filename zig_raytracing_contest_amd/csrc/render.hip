@@ -1023,8 +1023,8 @@ using WfFn = void (*)(const WfParams);
 // launch (80 VGPRs, no scratch access inside the cell walk).  7 waves put 2-3
 // spill reloads in the bounce walk and ran cfg3 at 1933 vs 2108 Mrays/s
 // (round 1); the 7-wave primary launch was within 0.2% of 6 in round 1 and
-// now reloads one spilled pair per cell step.  The timed instantiations are
-// exactly these two (tests/test_codegen.py reads them from zrt_timed_kernels).
+// now reloads one spilled pair per cell step.  tests/test_codegen.py checks
+// every instantiation zrt_timed_kernels names.
 constexpr int kWfMinWaves = 6;
 constexpr int kWfMinWaves0 = 6;
 // wf_park_kernel schedule: a test round once 12 lanes are parked, a shade +
@@ -1166,8 +1166,12 @@ extern "C" int zrt_device_count(int* count) {
 extern "C" const char* zrt_timed_kernels(void) {
 #define ZRT_STR2(x) #x
 #define ZRT_STR(x) ZRT_STR2(x)
+    // the default launch set: primary wf_kernel, then per bounce the
+    // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
+    // the scene's OccX does not fit the LDS)
     static_assert(kWfMinWaves0 == 6 && kWfMinWaves == 6, "update the strings below");
-    return "wf_kernelILi" ZRT_STR(6) "ELb1EE,wf_kernelILi" ZRT_STR(6) "ELb0EE";
+    return "wf_kernelILi" ZRT_STR(6) "ELb1EE,wf_park_kernelILb0ELb1EE,wf_shade_kernelILb0EE,wf_kernelILi" ZRT_STR(6)
+           "ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
