@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=None, help="override spp (NOT the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wall-clock", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=24.0)
     return ap.parse_args()
 
 
@@ -158,6 +158,8 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
             m = re.search(r"Done in (\S+)", log)
             done.append(parse_duration_ms(m.group(1)) if m else float("nan"))
         rays = re.search(r"Rays: .*", log)
+        stages = {m.group(1).lower(): round(parse_duration_ms(m.group(2)), 2)
+                  for m in re.finditer(r"info: (\w+) in (\S+)", log) if m.group(1) != "Done"}
         out = {"wall_clock_ms": round(min(done), 2),
                "wall_clock": {"what": f"zrt CLI, contest stand-in as glTF, --height {cfgd['height']} "
                                       f"--camera '{cfgd['camera']}', config.json num_samples "
@@ -165,7 +167,8 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
                                       "'Done in' (main.zig:78 -> :142), min of "
                                       f"{reps} runs", "done_in_ms": [round(x, 2) for x in done],
                               "process_ms": [round(x, 2) for x in wall],
-                              "cli_rays": rays.group(0) if rays else None}}
+                              "cli_rays": rays.group(0) if rays else None,
+                              "stages_ms_last_run": stages}}
         if cpu:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as orc   # test infrastructure: the CPU leg only
