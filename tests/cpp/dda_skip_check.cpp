@@ -2,7 +2,8 @@
 // rays (including axis-aligned and exact-diagonal ones that produce crossing
 // ties), the skip walk must enter exactly the same cells of occupied bricks,
 // with bit-identical DDA state, as the cell-by-cell walk of Iterator.next
-// (DDA_STEP), and leave the grid at the same point.
+// (DDA_STEP), and leave the grid at the same point.  And DDAW_STEP (the park
+// kernel's walk) must step exactly like DDA_STEP.
 //   g++ -O2 -std=c++17 -ffp-contract=off -I<csrc> dda_skip_check.cpp
 #include <cmath>
 #include <cstdio>
@@ -51,6 +52,29 @@ static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
 }
 
 static uint64_t g_texit_fails = 0;
+static uint64_t g_walk_fails = 0, g_walk_steps = 0;
+
+// DDAW_STEP (the park kernel's walk) against DDA_STEP, step by step: cells,
+// linear index, crossing flag, T_EXIT and the next crossing ts bit for bit
+static void walk_w(const GridK& k, Dda s) {
+    DdaW w;
+    ddaw_from(s, k, w);
+    for (int guard = 0; guard < 100000; ++guard) {
+        bool c1, c2;
+        float e1, e2;
+        DDA_STEP(s, k, 2, c1, e1);
+        DDAW_STEP(w, 2, c2, e2);
+        ++g_walk_steps;
+        const bool same = c1 == c2 && !memcmp(&e1, &e2, 4) && s.c0 == w.c0 && s.c1 == w.c1 && s.c2 == w.c2 &&
+                          s.lin == w.lin && !memcmp(&s.tn0, &w.tn0, 4) && !memcmp(&s.tn1, &w.tn1, 4) &&
+                          !memcmp(&s.tn2, &w.tn2, 4);
+        if (!same) {
+            ++g_walk_fails;
+            return;
+        }
+        if (e1 == kInf) return;
+    }
+}
 
 // product: skip unoccupied bricks whole; each skip's T_EXIT must be the exit
 // t of the last cell the cell walk passes in that brick (+inf at the grid
@@ -133,6 +157,7 @@ int main(int argc, char** argv) {
             if (!dda_init(g.bmin, g.bmax, g.res, g.cs, o, d, s)) continue;
             ++total;
             if (s.tn0 == s.tn1 || s.tn1 == s.tn2 || s.tn0 == s.tn2) ++ties;
+            walk_w(k, s);
             const auto a = walk_cells(g, k, s);
             const auto b = walk_skip(g, k, s, &skips);
             if (!(a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin()))) {
@@ -142,9 +167,11 @@ int main(int argc, char** argv) {
             }
         }
     }
-    fails += g_texit_fails;
-    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, \"fails\": %llu}\n",
+    fails += g_texit_fails + g_walk_fails;
+    printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, "
+           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"fails\": %llu}\n",
            (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
-           (unsigned long long)g_texit_fails, (unsigned long long)fails);
+           (unsigned long long)g_texit_fails, (unsigned long long)g_walk_steps, (unsigned long long)g_walk_fails,
+           (unsigned long long)fails);
     return fails ? 1 : 0;
 }

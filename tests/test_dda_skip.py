@@ -1,6 +1,7 @@
 """Host check of the exact empty-brick skip (csrc/dda.h BRICK_SKIP4) against
 the cell-by-cell Iterator.next walk (DDA_STEP): same cells of occupied
-bricks, bit-identical DDA state, same grid exit (tests/cpp/dda_skip_check.cpp).
+bricks, bit-identical DDA state, same grid exit (tests/cpp/dda_skip_check.cpp);
+and the park kernel's DDAW_STEP against DDA_STEP, step by step.
 The GPU kernels compile the same header; their images are checked against
 the oracle in test_gpu_parity.py."""
 import os
@@ -22,4 +23,6 @@ def test_brick_skip_matches_cell_walk(tmp_path):
                    check=True)
     r = subprocess.run([str(exe), "60", "6000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
-    assert '"fails": 0' in r.stdout
+    import json
+    res = json.loads(r.stdout)
+    assert res["fails"] == 0 and res["walk_fails"] == 0 and res["walk_steps"] > 100000, res

@@ -95,6 +95,60 @@ struct GridK {
         (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
     } while (0)
 
+// The park kernel's walk state: Dda with every per-axis quantity of a step
+// resolved at setup -- the exit cell e_a (0 or res_a - 1), the cell step s_a
+// (+1 or -1 mod 2^32) and the linear-index step l_a (+-1, +-str1, +-str2
+// mod 2^32; axis 0's is s_0) -- so a step selects them by axis instead of deriving them from
+// the sign bits and the grid constants (DDA_STEP: 44 VALU per step in the
+// r02m ISA, this: 29).  Same booleans, same f32 adds, same cells and T_EXIT
+// as DDA_STEP (tests/cpp/dda_skip_check.cpp compares the two step by step).
+struct DdaW {
+    float tn0, tn1, tn2, td0, td1, td2;
+    uint32_t c0, c1, c2;
+    uint32_t lin;
+    uint32_t e0, e1, e2;
+    uint32_t s0, s1, s2;      // s0 is also axis 0's linear-index step
+    uint32_t l1, l2;
+};
+ZHD void ddaw_from(const Dda& d, const GridK& g, DdaW& w) {
+    w.tn0 = d.tn0; w.tn1 = d.tn1; w.tn2 = d.tn2;
+    w.td0 = d.td0; w.td1 = d.td1; w.td2 = d.td2;
+    w.c0 = d.c0; w.c1 = d.c1; w.c2 = d.c2;
+    w.lin = d.lin;
+    const bool n0 = d.neg & 1u, n1 = (d.neg >> 1) & 1u, n2 = (d.neg >> 2) & 1u;
+    w.e0 = n0 ? 0u : g.rm0;
+    w.e1 = n1 ? 0u : g.rm1;
+    w.e2 = n2 ? 0u : g.rm2;
+    w.s0 = n0 ? 0xFFFFFFFFu : 1u;
+    w.s1 = n1 ? 0xFFFFFFFFu : 1u;
+    w.s2 = n2 ? 0xFFFFFFFFu : 1u;
+    w.l1 = n1 ? 0u - g.str1 : g.str1;
+    w.l2 = n2 ? 0u - g.str2 : g.str2;
+}
+#define DDAW_STEP(S, SH, CROSSED, T_EXIT)                                            \
+    do {                                                                             \
+        const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
+        const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
+        const bool a0_ = b01_ && b02_;                                               \
+        const bool a1_ = !b01_ && b12_;                                              \
+        const bool a2_ = !a0_ && !a1_;                                               \
+        const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
+        const float dt_ = a0_ ? (S).td0 : (a1_ ? (S).td1 : (S).td2);                 \
+        const uint32_t cc_ = a0_ ? (S).c0 : (a1_ ? (S).c1 : (S).c2);                 \
+        const uint32_t ec_ = a0_ ? (S).e0 : (a1_ ? (S).e1 : (S).e2);                 \
+        const uint32_t cn_ = cc_ + (a0_ ? (S).s0 : (a1_ ? (S).s1 : (S).s2));         \
+        (S).lin += a0_ ? (S).s0 : (a1_ ? (S).l1 : (S).l2);                           \
+        (CROSSED) = ((cc_ ^ cn_) >> (SH)) != 0u;                                     \
+        const float un_ = tc_ + dt_;                                                 \
+        (S).tn0 = a0_ ? un_ : t0_;                                                   \
+        (S).tn1 = a1_ ? un_ : t1_;                                                   \
+        (S).tn2 = a2_ ? un_ : t2_;                                                   \
+        (S).c0 = a0_ ? cn_ : (S).c0;                                                 \
+        (S).c1 = a1_ ? cn_ : (S).c1;                                                 \
+        (S).c2 = a2_ ? cn_ : (S).c2;                                                 \
+        (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
+    } while (0)
+
 // Empty-brick skip, 4^3 bricks (occ_shift 2): the state Iterator.next would
 // reach at the step that leaves the current brick, computed at once.  Axis
 // a's crossings form the sequence T_a(1) = tn_a, T_a(j+1) = T_a(j) + td_a

@@ -106,7 +106,7 @@ struct Stack {
 __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint32_t* occ, uint32_t c0,
                                                uint32_t c1, uint32_t c2) {
     const uint32_t s = p.occ_shift;
-    const uint32_t b = (c2 >> s) * p.occ_nb01 + (c1 >> s) * p.occ_nb0 + (c0 >> s);
+    const uint32_t b = __umul24(c2 >> s, p.occ_nb01) + __umul24(c1 >> s, p.occ_nb0) + (c0 >> s);   // nb <= 2^24 (context check)
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
@@ -169,10 +169,12 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr) {
     float nearest = kInf;
-    Dda s;
-    if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s)) return nearest;
+    Dda s0;
+    if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
     const uint32_t sh = p.occ_shift;
     const GridK gk = grid_consts(p);
+    DdaW s;
+    ddaw_from(s0, gk, s);
     bool occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
     for (;;) {
         if (STATS) ++n_cells;
@@ -199,7 +201,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         }
         bool crossed;
         float t_exit;
-        DDA_STEP(s, gk, sh, crossed, t_exit);
+        DDAW_STEP(s, sh, crossed, t_exit);
         if (nearest <= t_exit) break;                      // stage3.zig:179-182
         if (crossed) occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
     }
@@ -384,6 +386,7 @@ struct WfParams {
     // wf_park_kernel: exact per-cell occupancy blob (see OccX) and schedule
     const uint32_t* occx;
     uint32_t occx_words, occx_nbw, occx_moff, occx_nb0, occx_nb01;
+    uint32_t occx_ldsw;       // u32 words OccX takes in LDS (multiple of 4): entries + masks
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
 };
@@ -610,22 +613,41 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 // OccX (4^3-cell bricks): one bit per brick, the u16 number of occupied
 // bricks before each 32-brick word, one 64-bit cell mask per occupied brick
 // (+ one zero mask).
+// In LDS each 32-brick word sits beside its prefix as one 8-byte entry, so a
+// lookup is two dependent LDS reads: (bits, prefix), then the mask.
 struct OccX {
-    const uint32_t* bits;
-    const uint16_t* prefix;
+    const uint2* ent;                    // (brick bits, occupied bricks before the word)
     const unsigned long long* masks;
 };
 __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
-    const uint32_t wd = L.bits[b >> 5];
-    const uint32_t r = (uint32_t)L.prefix[b >> 5] + (uint32_t)__popc(wd & ((1u << (b & 31u)) - 1u));
+    const uint2 e = L.ent[b >> 5];
+    const uint32_t r = e.y + (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
     const unsigned long long m = L.masks[r];            // r <= occupied count: the zero mask at worst
-    return ((wd >> (b & 31u)) & 1u) ? m : 0ull;
+    return ((e.x >> (b & 31u)) & 1u) ? m : 0ull;
 }
-__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const Dda& s) {
-    return (s.c2 >> 2) * w.occx_nb01 + (s.c1 >> 2) * w.occx_nb0 + (s.c0 >> 2);
+// occx_mask for a brick index that may lie past the grid (a speculative
+// step beyond the exit cell): the word index is clamped into the blob, so
+// the read stays inside it; the result of such a lookup is never used
+__device__ __forceinline__ unsigned long long occx_mask_clamped(const OccX& L, uint32_t b, uint32_t nbw) {
+    const uint2 e = L.ent[min(b >> 5, nbw - 1u)];
+    const uint32_t r = e.y + (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
+    const unsigned long long m = L.masks[r];
+    return ((e.x >> (b & 31u)) & 1u) ? m : 0ull;
 }
-__device__ __forceinline__ uint32_t occx_bit(const Dda& s) {
-    return ((s.c2 & 3u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
+// brick index: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate),
+// exact because a grid of more than 2^24 bricks is rejected at context
+// creation (their bits would not fit the LDS)
+template <class D>
+__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const D& s) {
+    return __umul24(s.c2 >> 2, w.occx_nb01) + __umul24(s.c1 >> 2, w.occx_nb0) + (s.c0 >> 2);
+}
+// bit of cell (c0, c1, c2) in its brick's 64-bit mask, tested on the 32-bit
+// half that holds it (bit 5 of the index is bit 1 of c2)
+template <class D>
+__device__ __forceinline__ bool occx_cell(unsigned long long bm, const D& s) {
+    const uint32_t half = (s.c2 & 2u) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
+    const uint32_t k = ((s.c2 & 1u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
+    return (half >> k) & 1u;
 }
 
 // A parked lane's cell range [begin, end) is loaded by LDS-DMA into its
@@ -636,10 +658,27 @@ __device__ __forceinline__ uint32_t occx_bit(const Dda& s) {
 // r02k ISA).  Nothing orders an LDS read behind a pending LDS-DMA but the
 // wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
 constexpr int kParkWaves = kParkBlock / 64;
+//
+// Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
+// a store whose VGPR operands are read late, so whenever the register
+// allocator reuses the address registers inside the walk it guards the reuse
+// with a vmcnt(0) there -- every step then waits for the range load just
+// issued (r02p ISA: the two-step walk got one after a register shuffle).
+// The address is read when the instruction issues; the only consumer of the
+// data is the test round, behind its explicit vmcnt(0), and the kernel drains
+// vmcnt before it ends.
 __device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t lin, uint32_t* rng) {
     const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells) + 2ull * lin;
-    __builtin_amdgcn_global_load_lds(c, rng, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds(c + 1, rng + 64, 4, 0, 0);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rng);
+    // (an instruction offset would move the LDS destination too: the end
+    // word gets its own address)
+    asm volatile("s_mov_b32 m0, %2\n\t"
+                 "global_load_lds_dword %0, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %1, off"
+                 :
+                 : "v"(c), "v"(c + 1), "s"(m0)
+                 : "memory", "m0");
 }
 
 // Per-wave LDS of the test rounds.
@@ -694,15 +733,21 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     __shared__ double s_zig[514];
     __shared__ uint32_t s_rng[kParkWaves * 128];            // LDS-DMA range slots
     uint32_t* const rng_slot = s_rng + 128u * (threadIdx.x >> 6);
-    for (uint32_t i = threadIdx.x; i < w.occx_words; i += blockDim.x) s_dyn[i] = w.occx[i];
+    // OccX into LDS: (bits, prefix) entries, then the masks
+    {
+        const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
+        uint2* ent = reinterpret_cast<uint2*>(s_dyn);
+        for (uint32_t i = threadIdx.x; i < w.occx_nbw; i += blockDim.x) ent[i] = make_uint2(w.occx[i], pre[i]);
+        for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
+            s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
+    }
     if (!SPLIT)
         for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     __syncthreads();
     OccX L;
-    L.bits = s_dyn;
-    L.prefix = reinterpret_cast<const uint16_t*>(s_dyn + w.occx_nbw);
-    L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + w.occx_moff);
-    ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + ((w.occx_words + 3u) & ~3u))[threadIdx.x >> 6];
+    L.ent = reinterpret_cast<const uint2*>(s_dyn);
+    L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + 2 * w.occx_nbw);
+    ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + w.occx_ldsw)[threadIdx.x >> 6];
     const double* zx = s_zig;
     const double* zf = s_zig + 257;
 
@@ -716,9 +761,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t grp = blockIdx.x & 7u, tried = 0;
     // the segment: ray, DDA state, current brick's cell mask, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    Dda s;
-    s.tn0 = s.tn1 = s.tn2 = s.td0 = s.td1 = s.td2 = 0.0f;
-    s.c0 = s.c1 = s.c2 = s.lin = s.neg = 0;
+    DdaW s;
+    memset(&s, 0, sizeof s);
     unsigned long long bm = 0ull;
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
@@ -791,9 +835,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             hidx = 0;
                             W.o[lane] = make_float4(o.x, o.y, o.z, 0.0f);
                             W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
-                            if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s)) {   // stage3.zig:153-156
+                            Dda s0;
+                            if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
+                                ddaw_from(s0, gk, s);
                                 bm = occx_mask(L, occx_brick(w, s));
-                                if ((bm >> occx_bit(s)) & 1ull) {
+                                if (occx_cell(bm, s)) {
                                     park_load_range(p, s.lin, rng_slot);
                                     st = kPark;
                                 } else {
@@ -819,17 +865,42 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             PARK_COUNT(3, 1);
             PARK_COUNT(4, __popcll(wk));
             if (st == kWalk) {
-                bool crossed;
-                float t_exit;
-                DDA_STEP(s, gk, 2u, crossed, t_exit);
-                if (nearest <= t_exit) {                           // stage3.zig:179-182
+                // two DDA steps per trip: both cells' brick lookups are
+                // issued before either is used, so the trip waits out one
+                // chain of LDS latencies for two cells; the second step is
+                // speculative and dropped when the first cell parks or ends
+                // the segment (its lookup then reads a clamped brick)
+                DdaW s1 = s;
+                bool cr1, cr2;
+                float te1, te2;
+                DDAW_STEP(s1, 2u, cr1, te1);
+                DdaW s2 = s1;
+                DDAW_STEP(s2, 2u, cr2, te2);
+                unsigned long long q1 = occx_mask_clamped(L, occx_brick(w, s1), w.occx_nbw);
+                unsigned long long q2 = occx_mask_clamped(L, occx_brick(w, s2), w.occx_nbw);
+                // both lookups complete here, ahead of the branches below
+                // (left alone, the compiler sinks the second into the branch
+                // that uses it and the two LDS chains run one after the other)
+                asm volatile("" : "+v"(q1), "+v"(q2));
+                const unsigned long long m1 = cr1 ? q1 : bm;
+                const unsigned long long m2 = cr2 ? q2 : m1;
+                bool pk = false;
+                if (nearest <= te1) {                              // stage3.zig:179-182
+                    st = kDone;
+                } else if (occx_cell(m1, s1)) {
+                    s = s1;
+                    bm = m1;
+                    pk = true;
+                } else if (nearest <= te2) {
                     st = kDone;
                 } else {
-                    if (crossed) bm = occx_mask(L, occx_brick(w, s));
-                    if ((bm >> occx_bit(s)) & 1ull) {
-                        park_load_range(p, s.lin, rng_slot);
-                        st = kPark;
-                    }
+                    s = s2;
+                    bm = m2;
+                    pk = occx_cell(m2, s2);
+                }
+                if (pk) {                                          // one issue point per trip
+                    park_load_range(p, s.lin, rng_slot);
+                    st = kPark;
                 }
             }
         }
@@ -837,8 +908,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         // ---- test round: the parked lanes' cells, all pairs over all lanes
         if (__ballot(st == kPark) != 0ull) {
             __builtin_amdgcn_s_waitcnt(0x3f70);                    // vmcnt(0): the ranges landed
+            const bool ready = st == kPark;
             const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane];
-            const uint32_t n = st == kPark ? re - rb : 0u;
+            const uint32_t n = ready ? re - rb : 0u;
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
             PARK_COUNT(5, 1);
@@ -886,10 +958,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     hv = uv.y;
                 }
             }
-            if (st == kPark) st = kWalk;                           // the cell is done: step out of it next
+            if (ready) st = kWalk;                                 // the cell is done: step out of it next
         }
         PARK_STAMP(2);
     }
+    __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
 #ifdef ZRT_SWEEP
@@ -1342,6 +1415,10 @@ static void occx_layout(uint64_t nbw, uint64_t occupied, uint64_t* moff, uint64_
     *moff = (nbw + pw + 1) & ~1ull;
     *words = *moff + 2 * (occupied + 1);
 }
+// u32 words of the LDS copy: 8-byte (bits, prefix) entries, then the masks
+static uint64_t occx_lds_words(uint64_t nbw, uint64_t moff, uint64_t words) {
+    return (2 * nbw + (words - moff) + 3) & ~3ull;
+}
 
 // Brick occupancy (4^3-cell bricks: 4 KB of bits for a 128^3 grid, round 1's
 // best) and OccX, from the host cells or (host_cells null) from c->d_cells on
@@ -1352,7 +1429,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     c->occ_shift = sh;
     for (int i = 0; i < 3; ++i) c->occ_nb[i] = (r[i] + (1u << sh) - 1) >> sh;
     const uint64_t nb = (uint64_t)c->occ_nb[0] * c->occ_nb[1] * c->occ_nb[2];
-    if (nb > (1ull << 24)) return ZRT_ERR_UNSUPPORTED;    // > 64 KB of brick bits: more than LDS holds
+    if (nb > (1ull << 24)) return ZRT_ERR_UNSUPPORTED;    // brick indices are 24-bit (__umul24)
     const uint64_t nbw = (nb + 31) / 32;
     c->occ_words = (uint32_t)nbw;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = c->occ_nb[i];
@@ -1381,7 +1458,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         HIP_TRY(hipMemcpy(c->d_occ, bits.data(), nbw * 4, hipMemcpyHostToDevice));
         uint64_t moff, words;
         occx_layout(nbw, run, &moff, &words);
-        c->occx_ok = run < 0xFFFF && words * 4 <= kOccxBudget;
+        c->occx_ok = run < 0xFFFF && occx_lds_words(nbw, moff, words) * 4 <= kOccxBudget;
         if (c->occx_ok) {
             std::vector<uint32_t> blob(words, 0u);
             memcpy(blob.data(), bits.data(), nbw * 4);
@@ -1420,7 +1497,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         (void)hipFree(d_n);
         HIP_TRY(le);
         occx_layout(nbw, run, &moff, &words);
-        c->occx_ok = run < 0xFFFF && words * 4 <= kOccxBudget;
+        c->occx_ok = run < 0xFFFF && occx_lds_words(nbw, moff, words) * 4 <= kOccxBudget;
         c->occx_words = (uint32_t)words;
         c->occx_nbw = (uint32_t)nbw;
         c->occx_moff = (uint32_t)moff;
@@ -1661,7 +1738,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 #ifdef ZRT_SWEEP
     if (const char* e = getenv("ZRT_PARK_BLOCK")) park_block = std::max(64, std::min(kParkBlock, atoi(e) / 64 * 64));
 #endif
-    const size_t lds_park = 16ull * ((c->occx_words + 3u) / 4u) + (size_t)(park_block / 64) * sizeof(ParkSlot);
+    const uint32_t occx_ldsw = (uint32_t)occx_lds_words(c->occx_nbw, c->occx_moff, c->occx_words);
+    const size_t lds_park = 4ull * occx_ldsw + (size_t)(park_block / 64) * sizeof(ParkSlot);
     auto grid_for = [&](const void* f, int threads, size_t lds, uint32_t* blocks) -> int {
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1737,6 +1815,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.T = (uint32_t)T;
             W.occx = c->d_occx;
             W.occx_words = c->occx_words;
+            W.occx_ldsw = occx_ldsw;
             W.occx_nbw = c->occx_nbw;
             W.occx_moff = c->occx_moff;
             W.occx_nb0 = c->occx_nb[0];
