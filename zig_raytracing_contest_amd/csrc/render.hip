@@ -658,6 +658,7 @@ __device__ __forceinline__ bool occx_cell(unsigned long long bm, const D& s) {
 // r02k ISA).  Nothing orders an LDS read behind a pending LDS-DMA but the
 // wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
 constexpr int kParkWaves = kParkBlock / 64;
+constexpr uint32_t kParkChunk = 64;    // queue entries per work atomic of a park wave
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
 // a store whose VGPR operands are read late, so whenever the register
@@ -759,6 +760,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t st = kIdle;
     bool more = true;
     uint32_t grp = blockIdx.x & 7u, tried = 0;
+    uint32_t cb = 0, ce = 0, cgrp = 0;     // the wave's current chunk of queue entries
     // the segment: ray, DDA state, current brick's cell mask, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     DdaW s;
@@ -807,15 +809,26 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // per step)
                 __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
-            const uint64_t idle = __ballot(st == kIdle);
-            if (more && idle != 0ull) {
-                uint32_t base = 0, lim = 0;
-                more = wf_fetch<PRIMARY>(w, (uint32_t)__popcll(idle), grp, tried, base, lim);
-                if (more && st == kIdle) {
-                    const uint32_t j = base + (uint32_t)__popcll(idle & below);
-                    if (j < lim) {
-                        qi = ent_index<PRIMARY>(p, grp, j);
-                        reg = grp;
+            // idle lanes take entries of the wave's chunk [cb, ce) of group
+            // cgrp, a new chunk of kParkChunk entries once it is used up: one
+            // returning atomic per chunk instead of one per refill round
+            uint64_t idle = __ballot(st == kIdle);
+            while (idle != 0ull && (ce > cb || more)) {
+                if (cb == ce) {
+                    uint32_t base = 0, lim = 0;
+                    more = wf_fetch<PRIMARY>(w, kParkChunk, grp, tried, base, lim);
+                    if (!more) break;
+                    cb = base;
+                    ce = min(base + kParkChunk, lim);
+                    cgrp = grp;
+                }
+                const uint32_t take = min((uint32_t)__popcll(idle), ce - cb);
+                const uint32_t rank = (uint32_t)__popcll(idle & below);
+                if (st == kIdle && rank < take) {
+                    {
+                        const uint32_t j = cb + rank;
+                        qi = ent_index<PRIMARY>(p, cgrp, j);
+                        reg = cgrp;
                         uint32_t depth;
                         if (PRIMARY) {
                             Rng rng0;
@@ -851,6 +864,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                         }
                     }
                 }
+                cb += take;
+                idle = __ballot(st == kIdle);
             }
             PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
