@@ -77,3 +77,20 @@ def test_spill_check_sees_walk_spills():
     assert loops and max(s for _, _, s in loops) == 1
     clean = [l for l in lines if "scratch" not in l[1]]
     assert max(s for _, _, s in sc.walk_spills(clean)) == 0
+
+
+def test_park_kernel_m0_only_feeds_the_range_dma(code):
+    """park_load_range sets M0 in inline asm, which cannot declare M0
+    clobbered (reserved): the park kernels must not use M0 for anything else,
+    and every LDS-DMA must follow its own M0 write."""
+    sc, ks = code
+    import re
+    names = [n for n in ks if "wf_park_kernel" in n]
+    assert names
+    for n in names:
+        ins = [re.sub(r"\s*//.*", "", t).strip() for _, t in ks[n]]
+        for i, t in enumerate(ins):
+            if re.search(r"\bm0\b", t):
+                assert t.startswith(("s_mov_b32 m0,", "s_add_u32 m0, m0, 0x100")), (n, t)
+            if t.startswith("global_load_lds"):
+                assert any(re.search(r"\bm0\b", x) for x in ins[max(0, i - 3):i]), (n, i, ins[i - 3:i + 1])

@@ -667,7 +667,10 @@ constexpr uint32_t kParkChunk = 64;    // queue entries per work atomic of a par
 // issued (r02p ISA: the two-step walk got one after a register shuffle).
 // The address is read when the instruction issues; the only consumer of the
 // data is the test round, behind its explicit vmcnt(0), and the kernel drains
-// vmcnt before it ends.
+// vmcnt before it ends.  M0 cannot be declared clobbered (a reserved
+// register: the clobber is ignored), so nothing else in the park kernel may
+// rely on it: tests/test_codegen.py checks that every M0 access in its code
+// object is this sequence.
 __device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t lin, uint32_t* rng) {
     const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells) + 2ull * lin;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rng);
@@ -679,7 +682,7 @@ __device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t l
                  "global_load_lds_dword %1, off"
                  :
                  : "v"(c), "v"(c + 1), "s"(m0)
-                 : "memory", "m0");
+                 : "memory");
 }
 
 // Per-wave LDS of the test rounds.
