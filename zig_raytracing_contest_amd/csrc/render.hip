@@ -1110,14 +1110,15 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restric
 using TraceFn = void (*)(const TraceParams);
 using WfFn = void (*)(const WfParams);
 
-// wf_kernel occupancy (waves per SIMD, __launch_bounds__): 6 for every
-// launch (80 VGPRs, no scratch access inside the cell walk).  7 waves put 2-3
-// spill reloads in the bounce walk and ran cfg3 at 1933 vs 2108 Mrays/s
-// (round 1); the 7-wave primary launch was within 0.2% of 6 in round 1 and
-// now reloads one spilled pair per cell step.  tests/test_codegen.py checks
-// every instantiation zrt_timed_kernels names.
+// wf_kernel occupancy (waves per SIMD, __launch_bounds__).  The primary
+// launch at 7 (72 VGPRs, no scratch access inside the cell walk): r02ah, one
+// box, cfg3 64 spp at 5 / 6 / 7 / 8 waves 3127 / 3155 / 3197 / 3193 Mrays/s
+// (8 reloads spills inside the walk).  The lane-walk bounce launches
+// (ZRT_FLAG_LANE_WALK) at 6: 7 waves put 2-3 spill reloads in that walk and
+// ran cfg3 at 1933 vs 2108 (round 1).  tests/test_codegen.py checks every
+// instantiation zrt_timed_kernels names.
 constexpr int kWfMinWaves = 6;
-constexpr int kWfMinWaves0 = 6;
+constexpr int kWfMinWaves0 = 7;
 // wf_park_kernel schedule: a test round once 12 lanes are parked, a shade +
 // refill round once 16 lanes are finished (cfg3 64 spp sweep, r02d: T 4-16 x
 // R 8/16/32; T 12 R 16 3110 Mrays/s, T 8-16 R 16 within 1.3%, R 8 -15%,
@@ -1260,8 +1261,8 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    static_assert(kWfMinWaves0 == 6 && kWfMinWaves == 6, "update the strings below");
-    return "wf_kernelILi" ZRT_STR(6) "ELb1EE,wf_park_kernelILb0ELb1EE,wf_shade_kernelILb0EE,wf_kernelILi" ZRT_STR(6)
+    static_assert(kWfMinWaves0 == 7 && kWfMinWaves == 6, "update the strings below");
+    return "wf_kernelILi" ZRT_STR(7) "ELb1EE,wf_park_kernelILb0ELb1EE,wf_shade_kernelILb0EE,wf_kernelILi" ZRT_STR(6)
            "ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
