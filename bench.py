@@ -303,8 +303,8 @@ def main():
             "roofline": {"bound": "hbm", "limiter": "latency", "achieved": round(achieved, 1),
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                          "traffic": None,
-                         "kernel": "trace launches: wf_kernel<7,true> (primary), wf_park_kernel<false,true> + "
-                                   "wf_shade_kernel<false> (each bounce)",
+                         "kernel": "trace launches: wf_kernel<7,true> (primary), wf_park_kernel + "
+                                   "wf_shade_kernel (each bounce)",
                          "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                          "alg_GB_per_launch": round(per_launch / 1e9, 3)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",

@@ -111,8 +111,7 @@ typedef struct zrt_render_config {
 
 #define ZRT_FLAG_COUNT_STATS  0x1u   /* count cells/tests/hits (slower kernel variant) */
 #define ZRT_FLAG_LANE_WALK    0x2u   /* every launch walks + tests per lane (no park kernel) */
-#define ZRT_FLAG_PARK_PRIMARY 0x4u   /* the primary launch uses the park kernel too */
-#define ZRT_FLAG_PARK_INLINE  0x8u   /* park launches shade inline (no separate shade kernel) */
+/* 0x4, 0x8: reserved (round-2 kernel variants that were measured slower and removed) */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */

@@ -235,12 +235,9 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 
 
 # The timed kernels (no counting build) against the oracle on every scene:
-# the default (wf_kernel primary launch, park kernel bounces), per-lane
-# walks everywhere (the fallback when OccX does not fit), the park kernel on
-# every launch.
-MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("park-all", native.FLAG_PARK_PRIMARY),
-         ("park-inline", native.FLAG_PARK_INLINE),
-         ("park-all-inline", native.FLAG_PARK_PRIMARY | native.FLAG_PARK_INLINE)]
+# the default (wf_kernel primary launch, park + shade kernels for the
+# bounces) and per-lane walks everywhere (the fallback when OccX does not fit).
+MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK)]
 
 
 @pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])
@@ -319,7 +316,7 @@ for name, cam_name, h, spp in (("contest", "Camera 1", 54, 2), ("sponza", None, 
     c = soup.camera(cam_name)
     cam = camera_for(soup, cam_name, None if c.aspect else h, h)
     rs = RenderScene(soup, device=0)
-    img, _ = rs.render(cam, num_samples=spp, max_bounce=4, flags=native.FLAG_PARK_PRIMARY)
+    img, _ = rs.render(cam, num_samples=spp, max_bounce=4)
     rs.close()
     ocam = orc.camera_from_matrix(c.matrix, c.yfov, c.aspect, None if c.aspect else h, h)
     rgb, _, _ = orc.OracleScene(soup).render(ocam, spp, 4, orc.RNG_PATH, 0, 16)

@@ -730,11 +730,9 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 #define PARK_COUNT(k, v) do { } while (0)
 #endif
 
-template <bool PRIMARY, bool SPLIT>
 __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    __shared__ double s_zig[514];
     __shared__ uint32_t s_rng[kParkWaves * 128];            // LDS-DMA range slots
     uint32_t* const rng_slot = s_rng + 128u * (threadIdx.x >> 6);
     // OccX into LDS: (bits, prefix) entries, then the masks
@@ -745,15 +743,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
             s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
     }
-    if (!SPLIT)
-        for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     __syncthreads();
     OccX L;
     L.ent = reinterpret_cast<const uint2*>(s_dyn);
     L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + 2 * w.occx_nbw);
     ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + w.occx_ldsw)[threadIdx.x >> 6];
-    const double* zx = s_zig;
-    const double* zf = s_zig + 257;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
@@ -771,45 +765,25 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     unsigned long long bm = 0ull;
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
-    // the path: entry index (primary item / queue index) and its region
-    uint32_t qi = 0, reg = 0;
-    uint32_t n_seg = 0;
+    uint32_t qi = 0;                       // the path's queue entry
     PARK_PROF_DECL
 
     for (;;) {
-        // ---- shade + refill round, once enough lanes are finished or idle
+        // ---- hit records + refill round, once enough lanes are finished or idle
         const uint64_t busy = __ballot(st == kWalk || st == kPark);
         if ((uint32_t)(64 - __popcll(busy)) >= refill_min || busy == 0ull) {
             PARK_COUNT(8, 1);
             PARK_COUNT(9, __popcll(__ballot(st == kDone)));
-            if (SPLIT && __ballot(st == kDone) != 0ull) {
-                // the hit record for wf_shade_kernel; then drain the stores
-                // (see below)
+            if (__ballot(st == kDone) != 0ull) {
+                // the hit record for wf_shade_kernel; then drain the stores:
+                // otherwise the compiler guards the walk loop's reuse of their
+                // data registers with a vmcnt(0) INSIDE the loop, which then
+                // also waits for the previous step's range load, every step
+                // (r02f ISA; walk 1304 cycles per step)
                 if (st == kDone) {
                     w.hit[qi] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
                     st = kIdle;
                 }
-                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
-            }
-            if (!SPLIT && __ballot(st == kDone) != 0ull) {
-                bool cont = false;
-                uint32_t item = 0, depth = 0, slot = 0, mask = 0;
-                Rng rng;
-                rng.s = 0;
-                if (st == kDone) {                                 // stage3.zig:195-219
-                    path_state<PRIMARY>(w, qi, item, depth, slot, rng, mask);
-                    ++n_seg;
-                    v3 Lr = mk(0, 0, 0);
-                    cont = shade_segment(w, zx, zf, item, nearest, hu, hv, hidx, o, d, depth, slot, rng, mask, Lr);
-                    if (!cont) w.term[item] = make_float4(Lr.x, Lr.y, Lr.z, __uint_as_float(mask));
-                    st = kIdle;
-                }
-                wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, reg);
-                // drain the stores here: otherwise the compiler guards the
-                // walk loop's reuse of their data registers with a vmcnt(0)
-                // INSIDE the loop, which then also waits for the previous
-                // step's range load, every step (r02f ISA; walk 1304 cycles
-                // per step)
                 __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
             // idle lanes take entries of the wave's chunk [cb, ce) of group
@@ -819,7 +793,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             while (idle != 0ull && (ce > cb || more)) {
                 if (cb == ce) {
                     uint32_t base = 0, lim = 0;
-                    more = wf_fetch<PRIMARY>(w, kParkChunk, grp, tried, base, lim);
+                    more = wf_fetch<false>(w, kParkChunk, grp, tried, base, lim);
                     if (!more) break;
                     cb = base;
                     ce = min(base + kParkChunk, lim);
@@ -829,23 +803,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const uint32_t rank = (uint32_t)__popcll(idle & below);
                 if (st == kIdle && rank < take) {
                     {
-                        const uint32_t j = cb + rank;
-                        qi = ent_index<PRIMARY>(p, cgrp, j);
-                        reg = cgrp;
-                        uint32_t depth;
-                        if (PRIMARY) {
-                            Rng rng0;
-                            camera_ray(p, qi, rng0, o, d);
-                            depth = p.max_bounce;
-                        } else {
-                            const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
-                            o = mk(qa.x, qa.y, qa.z);
-                            d = mk(qb.x, qb.y, qb.z);
-                            depth = __float_as_uint(qb.w) & 0xFFFFu;
-                        }
-                        if (PRIMARY && depth == 0u) {              // max_bounce 0: black, nothing traced
-                            if (!SPLIT) w.term[qi] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        } else {
+                        qi = ent_index<false>(p, cgrp, cb + rank);
+                        const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
+                        o = mk(qa.x, qa.y, qa.z);
+                        d = mk(qb.x, qb.y, qb.z);
+                        {                                          // queued paths have depth >= 1
                             nearest = kInf;
                             hu = hv = 0.0f;
                             hidx = 0;
@@ -981,8 +943,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         PARK_STAMP(2);
     }
     __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
-    const unsigned long long s0 = wave_sum(n_seg);
-    if (lane == 0) atomicAdd(&p.stats[0], s0);
 #ifdef ZRT_SWEEP
     if (lane == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
@@ -993,7 +953,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 // after traceRay, stage3.zig:195-219) over the hit records wf_park_kernel
 // wrote, one lane per path with every lane of the wave busy, appending the
 // continuing paths to the next queue.  Same XCD group order as the trace.
-template <bool PRIMARY>
 __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -1009,7 +968,7 @@ __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w)
     ws.fetch8 = w.fetch8s;
     for (;;) {
         uint32_t base = 0, lim = 0;
-        if (!wf_fetch<PRIMARY>(ws, 64u, grp, tried, base, lim)) break;
+        if (!wf_fetch<false>(ws, 64u, grp, tried, base, lim)) break;
         const uint32_t j = base + lane;
         bool cont = false;
         uint32_t item = 0, depth = 0, slot = 0, mask = 0;
@@ -1017,23 +976,17 @@ __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w)
         Rng rng;
         rng.s = 0;
         if (j < lim) {
-            const uint32_t i = ent_index<PRIMARY>(p, grp, j);
-            if (PRIMARY) {
-                camera_ray(p, i, rng, o, d);
-                item = i;
-                depth = p.max_bounce;
-            } else {
-                const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
-                o = mk(a.x, a.y, a.z);
-                item = __float_as_uint(a.w);
-                d = mk(b.x, b.y, b.z);
-                depth = __float_as_uint(b.w) & 0xFFFFu;
-                slot = __float_as_uint(b.w) >> 16;
-                rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-                mask = __float_as_uint(c.z);
-            }
+            const uint32_t i = ent_index<false>(p, grp, j);
+            const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
+            o = mk(a.x, a.y, a.z);
+            item = __float_as_uint(a.w);
+            d = mk(b.x, b.y, b.z);
+            depth = __float_as_uint(b.w) & 0xFFFFu;
+            slot = __float_as_uint(b.w) >> 16;
+            rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+            mask = __float_as_uint(c.z);
             v3 L = mk(0, 0, 0);
-            if (depth != 0) {                  // max_bounce 0: black, nothing traced
+            {                                  // queued paths have depth >= 1
                 ++n_seg;
                 const float4 h = w.hit[i];
                 cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot,
@@ -1262,8 +1215,7 @@ extern "C" const char* zrt_timed_kernels(void) {
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
     static_assert(kWfMinWaves0 == 7 && kWfMinWaves == 6, "update the strings below");
-    return "wf_kernelILi" ZRT_STR(7) "ELb1EE,wf_park_kernelILb0ELb1EE,wf_shade_kernelILb0EE,wf_kernelILi" ZRT_STR(6)
-           "ELb0EE";
+    return "wf_kernelILi" ZRT_STR(7) "ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(6) "ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
@@ -1726,30 +1678,22 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         c->ev_trace.push_back(e);
     }
 
-    // Kernel per launch: the park kernel for the bounce launches (incoherent
-    // rays) when the scene's OccX fits the LDS budget, wf_kernel for the
-    // primary launch (coherent 8x8-pixel waves: 22 vs 42 ms at cfg3 64 spp,
-    // r02d).  ZRT_FLAG_LANE_WALK: wf_kernel for every launch (the fallback);
-    // ZRT_FLAG_PARK_PRIMARY: the park kernel for the primary launch too.
-    const bool can_park = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK);
-    const bool park_next = can_park;
-    const bool park_first = can_park && (cfg->flags & ZRT_FLAG_PARK_PRIMARY);
+    // Kernel per launch: the park kernel (traces, writes hit records) +
+    // wf_shade_kernel for the bounce launches (incoherent rays) when the
+    // scene's OccX fits the LDS budget, wf_kernel for the primary launch
+    // (coherent 8x8-pixel waves: 22 vs 42 ms for the park kernel at cfg3 64
+    // spp, r02d).  ZRT_FLAG_LANE_WALK: wf_kernel for every launch (round 1's
+    // path, and the fallback).
+    const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK);
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
 #ifdef ZRT_SWEEP
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
-    // split: the park kernel traces only (hit records), wf_shade_kernel
-    // shades with whole waves; ZRT_FLAG_PARK_INLINE: the park kernel shades
-    // in its refill rounds
-    const bool split = !(cfg->flags & ZRT_FLAG_PARK_INLINE);
-    const WfFn f_first = park_first ? (split ? (WfFn)wf_park_kernel<true, true> : (WfFn)wf_park_kernel<true, false>)
-                                    : kWfPrimary;
-    const WfFn f_next = park_next ? (split ? (WfFn)wf_park_kernel<false, true> : (WfFn)wf_park_kernel<false, false>)
-                                  : kWfBounce;
-    const WfFn s_first = (WfFn)wf_shade_kernel<true>, s_next = (WfFn)wf_shade_kernel<false>;
-    const bool shade_first = park_first && split, shade_next = park_next && split;
-    if ((shade_first || shade_next) && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
+    const WfFn f_first = kWfPrimary;
+    const WfFn f_next = park_next ? (WfFn)wf_park_kernel : kWfBounce;
+    const WfFn s_next = (WfFn)wf_shade_kernel;
+    if (park_next && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
@@ -1768,9 +1712,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         return ZRT_OK;
     };
     uint32_t grid_first = 0, grid_next = 0, grid_count = 0, grid_shade = 0;
-    const int thr_first = park_first ? park_block : kTraceThreads;
+    const int thr_first = kTraceThreads;
     const int thr_next = park_next ? park_block : kTraceThreads;
-    const size_t lds_first = park_first ? lds_park : lds_wf, lds_next = park_next ? lds_park : lds_wf;
+    const size_t lds_first = lds_wf, lds_next = park_next ? lds_park : lds_wf;
     if (counting) {
         if ((rc = grid_for((const void*)cfn, kTraceThreads, lds_wf, &grid_count)) != ZRT_OK) return rc;
     } else {
@@ -1855,8 +1799,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 else
                     hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, c->stream, W);
                 HIP_TRY(hipGetLastError());
-                if (k == 0 ? shade_first : shade_next) {     // same bounce, shading half
-                    hipLaunchKernelGGL(k == 0 ? s_first : s_next, dim3(grid_shade), dim3(kTraceThreads), 0, c->stream, W);
+                if (k > 0 && park_next) {                    // same bounce, shading half
+                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), 0, c->stream, W);
                     HIP_TRY(hipGetLastError());
                 }
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));

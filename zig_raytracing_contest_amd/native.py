@@ -19,7 +19,7 @@ ZRT_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime error",
           -4: "out of memory", -5: "unsupported configuration", -6: "I/O error",
           -7: "parse error", -8: "not found", -9: "camera/output size rules violated"}
-FLAG_COUNT_STATS, FLAG_LANE_WALK, FLAG_PARK_PRIMARY, FLAG_PARK_INLINE = 0x1, 0x2, 0x4, 0x8
+FLAG_COUNT_STATS, FLAG_LANE_WALK = 0x1, 0x2
 
 PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
