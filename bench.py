@@ -71,7 +71,11 @@ def traffic_for(config, kernel):
     summary for this workload (tools/pmc_traffic.py over rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 corrections there)."""
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json"))):
+    # newest round tag last: r01 < r01i < r02e < r02m < r02aj (length, then name)
+    def tag_key(f):
+        t = os.path.basename(f).split("_traffic_")[0]
+        return (len(t), t)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")), key=tag_key):
         try:
             with open(f) as fh:
                 t = json.load(fh)
