@@ -9,7 +9,8 @@ upload, and the device build straight into the context):
 - degenerate triangles (zero area, collinear, repeated vertices) mixed into a
   mesh: Moller-Trumbore's det == 0 path (linalg.zig:683-722) and the SAT
   build (linalg.zig:516-563);
-- a one-triangle scene, grid resolutions 1x1x1 and non-cubic;
+- a one-triangle scene, grid resolutions 1x1x1 and non-cubic, and grids
+  large enough for coarser occupancy bricks (300x260x280, 640x256x512);
 - max_bounce 0 (primary rays only).
 """
 import dataclasses
@@ -78,7 +79,11 @@ CASES = [("sphere", 1, 1, 3, 4, (128, 128, 128)),
          ("cornell_inside", 64, 48, 2, 4, (128, 128, 128)),
          ("cornell_inside", 64, 48, 2, 4, (31, 64, 17)),
          ("cornell_inside", 64, 48, 4, 0, (128, 128, 128)),
-         ("sky_only", 32, 24, 2, 4, (128, 128, 128))]
+         ("sky_only", 32, 24, 2, 4, (128, 128, 128)),
+         # grids whose 4^3-brick bits exceed wf_kernel's LDS share: coarser
+         # occupancy bricks (8^3, 16^3), and no OccX (the lane-walk fallback)
+         ("cornell_inside", 48, 40, 2, 4, (300, 260, 280)),
+         ("sphere", 32, 24, 1, 3, (640, 256, 512))]
 
 
 @pytest.fixture(scope="module")

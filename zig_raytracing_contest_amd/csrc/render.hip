@@ -1391,29 +1391,56 @@ static uint64_t occx_lds_words(uint64_t nbw, uint64_t moff, uint64_t words) {
     return (2 * nbw + (words - moff) + 3) & ~3ull;
 }
 
-// Brick occupancy (4^3-cell bricks: 4 KB of bits for a 128^3 grid, round 1's
-// best) and OccX, from the host cells or (host_cells null) from c->d_cells on
-// the device; then the work counters.
+// Brick occupancy and OccX, from the host cells or (host_cells null) from
+// c->d_cells on the device; then the work counters.
+//  * OccX (the park kernel) is built on 4^3-cell bricks and used when it fits
+//    the LDS budget.
+//  * wf_kernel's brick bits sit in LDS beside 7 waves' worth of workgroups:
+//    4^3-cell bricks (4 KB of bits for a 128^3 grid, round 1's best) while
+//    the bits take at most kOccLdsMax bytes, coarser bricks (8^3, 16^3, ...:
+//    OR of the 4^3 ones) for larger grids -- result-invariant, an empty brick
+//    only lets the walk skip the range loads of its cells.
+constexpr uint64_t kOccLdsMax = 16 << 10;
+
+__global__ __launch_bounds__(kBlock) void occ_coarsen_kernel(const uint32_t* __restrict__ bits4, uint32_t nb0,
+                                                             uint32_t nb1, uint32_t nb, uint32_t dsh, uint32_t cn0,
+                                                             uint32_t cn01, uint32_t* __restrict__ out) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= nb || !((bits4[b >> 5] >> (b & 31u)) & 1u)) return;
+    const uint32_t bx = b % nb0, by = (b / nb0) % nb1, bz = b / (nb0 * nb1);
+    const uint32_t cb = (bz >> dsh) * cn01 + (by >> dsh) * cn0 + (bx >> dsh);
+    atomicOr(&out[cb >> 5], 1u << (cb & 31u));
+}
+
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     const uint32_t* r = c->grid.resolution;
-    const uint32_t sh = 2;
-    c->occ_shift = sh;
-    for (int i = 0; i < 3; ++i) c->occ_nb[i] = (r[i] + (1u << sh) - 1) >> sh;
-    const uint64_t nb = (uint64_t)c->occ_nb[0] * c->occ_nb[1] * c->occ_nb[2];
+    for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
+    const uint64_t nb = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
     if (nb > (1ull << 24)) return ZRT_ERR_UNSUPPORTED;    // brick indices are 24-bit (__umul24)
     const uint64_t nbw = (nb + 31) / 32;
-    c->occ_words = (uint32_t)nbw;
-    for (int i = 0; i < 3; ++i) c->occx_nb[i] = c->occ_nb[i];
-    HIP_TRY(hipMalloc((void**)&c->d_occ, nbw * 4));
+    uint32_t sh = 2;
+    auto words_at = [&](uint32_t k) {
+        const uint64_t n = (uint64_t)((r[0] + (1u << k) - 1) >> k) * ((r[1] + (1u << k) - 1) >> k) *
+                           ((r[2] + (1u << k) - 1) >> k);
+        return (n + 31) / 32;
+    };
+    while (words_at(sh) * 4 > kOccLdsMax) ++sh;
+    c->occ_shift = sh;
+    for (int i = 0; i < 3; ++i) c->occ_nb[i] = (r[i] + (1u << sh) - 1) >> sh;
+    c->occ_words = (uint32_t)words_at(sh);
+    HIP_TRY(hipMalloc((void**)&c->d_occ, 4ull * c->occ_words));
     if (host_cells) {
         std::vector<unsigned long long> mask(nb, 0ull);
+        std::vector<uint32_t> coarse(c->occ_words, 0u);
         for (uint32_t z = 0; z < r[2]; ++z)
             for (uint32_t y = 0; y < r[1]; ++y)
                 for (uint32_t x = 0; x < r[0]; ++x) {
                     const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
                     if (host_cells[2 * ci] < host_cells[2 * ci + 1]) {
-                        const uint64_t b = ((uint64_t)(z >> 2) * c->occ_nb[1] + (y >> 2)) * c->occ_nb[0] + (x >> 2);
+                        const uint64_t b = ((uint64_t)(z >> 2) * c->occx_nb[1] + (y >> 2)) * c->occx_nb[0] + (x >> 2);
                         mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
+                        const uint64_t cb = ((uint64_t)(z >> sh) * c->occ_nb[1] + (y >> sh)) * c->occ_nb[0] + (x >> sh);
+                        coarse[cb >> 5] |= 1u << (cb & 31);
                     }
                 }
         std::vector<uint32_t> bits(nbw, 0u);
@@ -1426,7 +1453,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                 if (mask[b]) { bits[wd] |= 1u << (b & 31); masks.push_back(mask[b]); ++run; }
         }
         masks.push_back(0ull);
-        HIP_TRY(hipMemcpy(c->d_occ, bits.data(), nbw * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
         uint64_t moff, words;
         occx_layout(nbw, run, &moff, &words);
         c->occx_ok = run < 0xFFFF && occx_lds_words(nbw, moff, words) * 4 <= kOccxBudget;
@@ -1454,13 +1481,21 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         c->d_occx = d_blob;            // freed with the context from here on
         HIP_TRY(hipMemsetAsync(d_blob, 0, words * 4, c->stream));
         hipLaunchKernelGGL(occx_mask_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                           c->d_cells, r[0], r[1], r[2], c->occ_nb[0], c->occ_nb[1], (uint32_t)nb, d_masks, d_blob);
+                           c->d_cells, r[0], r[1], r[2], c->occx_nb[0], c->occx_nb[1], (uint32_t)nb, d_masks, d_blob);
         hipLaunchKernelGGL(occx_pack_kernel, dim3(1), dim3(1024), 0, c->stream, (const uint32_t*)d_blob,
                            (uint32_t)nbw, (const unsigned long long*)d_masks,
                            reinterpret_cast<uint16_t*>(d_blob + nbw),
                            reinterpret_cast<unsigned long long*>(d_blob + moff), d_n);
-        const hipError_t le = hipGetLastError();
-        HIP_TRY(hipMemcpyAsync(c->d_occ, d_blob, nbw * 4, hipMemcpyDeviceToDevice, c->stream));
+        hipError_t le = hipGetLastError();
+        if (sh == 2) {
+            HIP_TRY(hipMemcpyAsync(c->d_occ, d_blob, nbw * 4, hipMemcpyDeviceToDevice, c->stream));
+        } else {
+            HIP_TRY(hipMemsetAsync(c->d_occ, 0, 4ull * c->occ_words, c->stream));
+            hipLaunchKernelGGL(occ_coarsen_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               c->stream, (const uint32_t*)d_blob, c->occx_nb[0], c->occx_nb[1], (uint32_t)nb, sh - 2u,
+                               c->occ_nb[0], c->occ_nb[0] * c->occ_nb[1], c->d_occ);
+            if (le == hipSuccess) le = hipGetLastError();
+        }
         uint32_t run = 0;
         HIP_TRY(hipMemcpyAsync(&run, d_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
