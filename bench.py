@@ -86,6 +86,34 @@ def traffic_for(config, kernel):
     return best
 
 
+def valu_for(config):
+    """VALU issue fraction per launch type (SURVEY.md d3's secondary figure)
+    from the newest committed SQ counter summary for this workload
+    (tools/gpu_r2round.sh: SQ_INSTS_VALU x 2 cycles / SIMD cycles)."""
+    files = glob.glob(os.path.join(ROOT, "profiles", "r02", f"r*_sq_counters_{config}_*.json"))
+    if not files:
+        return None
+    f = max(files, key=lambda x: (len(os.path.basename(x).split("_")[0]), os.path.basename(x)))
+    try:
+        with open(f) as fh:
+            d = json.load(fh)
+        return {"per_kernel": {k.rstrip("( "): v.get("_valu_issue_frac") for k, v in d["kernels"].items()},
+                "source": os.path.relpath(f, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_threads():
     """All CPUs this process may use (the reference's num_threads null =
     getCpuCount, main.zig:90), capped by OMP_NUM_THREADS when set: on the
@@ -123,7 +151,7 @@ def cpu_baseline(soup, cfg, target_s):
         spp = int(min(256, max(4, want_samples / npx)))
     dt, ctr, n = run(stride, spp)
     return {"value": round(float(ctr[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
-            "cores_available": avail, "kind": "port",
+            "cores_available": avail, "nproc": os.cpu_count(), "cpu_model": cpu_model(), "kind": "port",
             "sample": f"{n} pixels (every {stride}th of {cam.w}x{cam.h}) x {spp} spp, "
                       f"{int(ctr[0])} segments in {dt:.1f}s; oracle REF mode (Xoshiro256++ per "
                       f"thread, contiguous blocks, recursion), gcc -O3, {threads} threads "
@@ -313,7 +341,12 @@ def main():
                          "alg_GB_per_launch": round(per_launch / 1e9, 3)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},
+            # SURVEY.md d1's companion rate: w*h*spp per second of the timed frames
+            "msamples_per_s": round(cam.w * cam.h * spp * a.steps / elapsed / 1e6, 3),
         }
+        vc = valu_for(a.config) if spp == cfgd["spp"] else None
+        if vc:
+            out["roofline"]["valu_issue"] = vc
         tr = traffic_for(a.config, "wf_shade_kernel") if spp == cfgd["spp"] else None
         if tr:
             mem_gbs = tr[0] / 1e9 / avg_launch_s
