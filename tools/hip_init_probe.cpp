@@ -23,10 +23,15 @@ int main(int argc, char** argv) {
     void* h = dlopen(lib, RTLD_NOW);
     if (!h) { fprintf(stderr, "%s\n", dlerror()); return 2; }
     const double t3 = now_ms();
+    // grid_build.hip's module first (its hipCUB scans and sorts), then the
+    // rest of zrt_device_warmup (render.hip's module)
+    auto gwarm = (int (*)())dlsym(h, "_Z17grid_build_warmupv");
+    if (gwarm && gwarm() != 0) return 2;
+    const double t3b = now_ms();
     auto warm = (int (*)(int))dlsym(h, "zrt_device_warmup");
     if (!warm || warm(0) != 0) return 2;
     const double t4 = now_ms();
-    printf("{\"device_count_ms\": %.2f, \"context_ms\": %.2f, \"dlopen_ms\": %.2f, \"warmup_ms\": %.2f}\n", t1 - t0,
-           t2 - t1, t3 - t2, t4 - t3);
+    printf("{\"device_count_ms\": %.2f, \"context_ms\": %.2f, \"dlopen_ms\": %.2f, \"grid_module_ms\": %.2f, "
+           "\"warmup_rest_ms\": %.2f}\n", t1 - t0, t2 - t1, t3 - t2, t3b - t3, t4 - t3b);
     return 0;
 }

@@ -19,7 +19,7 @@
 //                        (stage2.zig:85-95);
 //   5. sat_kernel<1>     the same tests again; a hit takes a slot of its cell
 //                        (atomic, any order) and stores the key (cell, triangle);
-//   6. radix sort of the keys (hipcub): per cell, the refs in increasing
+//   6. radix sort of the keys (LSD, 8-bit digits, below): per cell, the refs in increasing
 //                        triangle order -- exactly the reference's fill order --
 //                        whatever the cell's size (a 1x1x1 grid is one cell of
 //                        every triangle);
@@ -32,8 +32,12 @@
 // microseconds of VALU); the passes over the 2 M cells (counts, scan, order,
 // cells: ~50 MB) and the baked arrays (~80 MB written) make it HBM-bound,
 // a few ms in total.  Costlier for the wall clock: the host<->device copies.
+//
+// The scans and the sort are this file's own (no hipCUB): hipCUB's scan and
+// radix-sort instantiations were 3.9 MB of the library's 4.2 MB of code
+// objects, and loading them on the first HIP call took 8-25 ms of the CLI's
+// wall clock on the GPU host (tools/hip_init_probe.cpp, r02ap / r02aq).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <new>
@@ -200,6 +204,182 @@ struct DevBufs {
 
 uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kB - 1) / kB); }
 
+// ---- exclusive scan, three passes over tiles of kScanTile items: per-tile
+// sums, their scan (one workgroup), then each tile scanned from its offset.
+// Integer sums: the same result for any tiling.
+constexpr int kScanItems = 8;
+constexpr uint32_t kScanTile = kB * kScanItems;
+
+// exclusive scan of one value per thread over the workgroup; total to *tot
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh, T* tot) {
+    const uint32_t tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < (uint32_t)kB; o <<= 1) {
+        const T add = tid >= o ? sh[tid - o] : T(0);
+        __syncthreads();
+        sh[tid] += add;
+        __syncthreads();
+    }
+    const T incl = sh[tid];
+    if (tot) *tot = sh[kB - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kB) void scan_tile_sums(const T* __restrict__ in, uint64_t n, T* __restrict__ sums) {
+    __shared__ T sh[kB];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    T v = 0;
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < n) v += in[base + k];
+    T tot;
+    (void)block_excl_scan(v, sh, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// one workgroup: the tile sums scanned in place (exclusive)
+template <typename T>
+__global__ __launch_bounds__(kB) void scan_sums(T* __restrict__ sums, uint32_t nt) {
+    __shared__ T sh[kB];
+    const uint32_t per = (nt + kB - 1) / kB;
+    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nt);
+    T v = 0;
+    for (uint32_t i = b0; i < b1; ++i) v += sums[i];
+    T run = block_excl_scan(v, sh, (T*)nullptr);
+    for (uint32_t i = b0; i < b1; ++i) {
+        const T x = sums[i];
+        sums[i] = run;
+        run += x;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kB) void scan_tiles(const T* __restrict__ in, uint64_t n, const T* __restrict__ sums,
+                                                 T* __restrict__ out) {
+    __shared__ T sh[kB];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    T x[kScanItems];
+    T v = 0;
+    for (int k = 0; k < kScanItems; ++k) {
+        x[k] = base + k < n ? in[base + k] : T(0);
+        v += x[k];
+    }
+    T run = block_excl_scan(v, sh, (T*)nullptr) + sums[blockIdx.x];
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < n) {
+            out[base + k] = run;
+            run += x[k];
+        }
+}
+
+// out[i] = in[0] + ... + in[i-1]; tmp: at least scan_tmp_items(n) T's
+uint64_t scan_tmp_items(uint64_t n) { return std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile); }
+template <typename T>
+hipError_t exclusive_scan(const T* in, T* out, uint64_t n, T* tmp, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint32_t nt = (uint32_t)scan_tmp_items(n);
+    hipLaunchKernelGGL(scan_tile_sums<T>, dim3(nt), dim3(kB), 0, st, in, n, tmp);
+    hipLaunchKernelGGL(scan_sums<T>, dim3(1), dim3(kB), 0, st, tmp, nt);
+    hipLaunchKernelGGL(scan_tiles<T>, dim3(nt), dim3(kB), 0, st, in, n, (const T*)tmp, out);
+    return hipGetLastError();
+}
+
+// ---- stable LSD radix sort of u64 keys, 8-bit digits.  Per pass: a digit
+// histogram per tile of kSortTile keys (digit-major, so the exclusive scan
+// of all of them gives each (digit, tile) its first output slot), then the
+// scatter: each tile walks its keys in index order, 256 at a time; a key's
+// slot is its (digit, tile) base + the keys of that digit already written
+// by the tile + those ahead of it in the same round (earlier waves, then
+// earlier lanes: the lanes of a wave with the same digit found by ballots
+// over the 8 digit bits).  Stable, so after the passes over the low 32 bits
+// (the triangle) and then the cell bits the keys are in (cell, triangle)
+// order -- the reference's fill order.
+constexpr int kSortRounds = 16;
+constexpr uint32_t kSortTile = kB * kSortRounds;
+constexpr int kWaves = kB / 64;
+
+__global__ __launch_bounds__(kB) void sort_hist_kernel(const unsigned long long* __restrict__ keys, uint32_t n,
+                                                       uint32_t shift, uint32_t nt, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortRounds; ++r) {
+        const uint32_t i = base + (uint32_t)r * kB + threadIdx.x;
+        if (i < n) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * nt + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kB) void sort_scatter_kernel(const unsigned long long* __restrict__ keys, uint32_t n,
+                                                          uint32_t shift, uint32_t nt, const uint32_t* __restrict__ off,
+                                                          unsigned long long* __restrict__ out) {
+    __shared__ uint32_t run[256];            // keys of each digit this tile has placed
+    __shared__ uint32_t wc[kWaves][256];     // this round: keys of each digit per wave
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    run[tid] = off[(size_t)tid * nt + blockIdx.x];
+    const uint32_t base = blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortRounds; ++r) {
+        for (int w = 0; w < kWaves; ++w) wc[w][tid] = 0;
+        __syncthreads();
+        const uint32_t i = base + (uint32_t)r * kB + tid;
+        const bool valid = i < n;
+        const unsigned long long key = valid ? keys[i] : 0ull;
+        const uint32_t d = (uint32_t)(key >> shift) & 255u;
+        // lanes of this wave holding a valid key with the same digit
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t m = __ballot(valid && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        if (valid && (peers & below) == 0ull) wc[wave][d] = (uint32_t)__popcll(peers);   // the digit's first lane
+        __syncthreads();
+        if (valid) {
+            uint32_t ahead = run[d];
+            for (int w = 0; w < (int)wave; ++w) ahead += wc[w][d];
+            out[ahead + (uint32_t)__popcll(peers & below)] = key;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+        for (int w = 0; w < kWaves; ++w) add += wc[w][tid];
+        run[tid] += add;
+        __syncthreads();
+    }
+}
+
+// sorts keys[0, n) on bits [0, nbits); the result ends in *keys or *alt
+// (returned through *result); tmp: 256 * tiles + scan_tmp_items of that
+hipError_t radix_sort(unsigned long long* keys, unsigned long long* alt, uint32_t n, uint32_t nbits, uint32_t* tmp,
+                      hipStream_t st, unsigned long long** result) {
+    const uint32_t nt = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
+    uint32_t* hist = tmp;
+    uint32_t* off = tmp + 256ull * nt;
+    uint32_t* stmp = off + 256ull * nt;
+    unsigned long long *a = keys, *b = alt;
+    for (uint32_t shift = 0; shift < nbits; shift += 8) {
+        hipLaunchKernelGGL(sort_hist_kernel, dim3(nt), dim3(kB), 0, st, (const unsigned long long*)a, n, shift, nt,
+                           hist);
+        hipError_t e = exclusive_scan<uint32_t>(hist, off, 256ull * nt, stmp, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(sort_scatter_kernel, dim3(nt), dim3(kB), 0, st, (const unsigned long long*)a, n, shift, nt,
+                           (const uint32_t*)off, b);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        std::swap(a, b);
+    }
+    *result = a;
+    return hipSuccess;
+}
+uint64_t radix_tmp_items(uint32_t n) {
+    const uint64_t nt = std::max<uint32_t>(1, (n + kSortTile - 1) / kSortTile);
+    return 512ull * nt + scan_tmp_items(256ull * nt);
+}
+
 }  // namespace
 
 namespace {
@@ -226,12 +406,9 @@ int build_on_device(const float* positions, const float* normals, const float* t
     // 1-2: candidates per triangle, scanned
     hipLaunchKernelGGL(cand_kernel, dim3(blocks_for(n + 1ull)), dim3(kB), 0, st, d_pos, n, g, d_range, d_cnt);
     GB_TRY(hipGetLastError());
-    size_t tmp_bytes = 0, need = 0;
-    GB_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, d_cnt, d_off, n + 1u, st));
-    uint8_t* d_tmp = nullptr;
-    GB_TRY(B.alloc(&d_tmp, need));
-    tmp_bytes = need;
-    GB_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_cnt, d_off, n + 1u, st));
+    unsigned long long* d_stmp64;
+    GB_TRY(B.alloc(&d_stmp64, scan_tmp_items(n + 1ull)));
+    GB_TRY(exclusive_scan<unsigned long long>(d_cnt, d_off, n + 1ull, d_stmp64, st));
     unsigned long long total = 0;
     GB_TRY(hipMemcpyAsync(&total, d_off + n, 8, hipMemcpyDeviceToHost, st));
     GB_TRY(hipStreamSynchronize(st));
@@ -249,15 +426,11 @@ int build_on_device(const float* positions, const float* normals, const float* t
     }
     unsigned long long refs64 = 0;
     GB_TRY(hipMemcpyAsync(&refs64, d_nrefs, 8, hipMemcpyDeviceToHost, st));
-    need = 0;
-    GB_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, d_count, d_first, ncells, st));
-    if (need > tmp_bytes) {
-        GB_TRY(B.alloc(&d_tmp, need));
-        tmp_bytes = need;
-    }
-    GB_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp, need, d_count, d_first, ncells, st));
+    uint32_t* d_stmp32;
+    GB_TRY(B.alloc(&d_stmp32, scan_tmp_items(ncells)));
+    GB_TRY(exclusive_scan<uint32_t>(d_count, d_first, ncells, d_stmp32, st));
     GB_TRY(hipStreamSynchronize(st));
-    if (refs64 > 0x7FFFFFFFull) return ZRT_ERR_UNSUPPORTED;   // hipcub item counts are int
+    if (refs64 > 0x7FFFFFFFull) return ZRT_ERR_UNSUPPORTED;   // u32 slots (refs of a 2^31-ref grid: 16 GB of Pos)
     const uint32_t refs = (uint32_t)refs64;
 
     // 5-6: fill, then the reference's order within each cell
@@ -273,17 +446,14 @@ int build_on_device(const float* positions, const float* normals, const float* t
         GB_TRY(hipGetLastError());
     }
     if (refs) {
-        int cell_bits = 1;
+        uint32_t cell_bits = 1;
         while (cell_bits < 31 && (1u << cell_bits) < ncells) ++cell_bits;
-        hipcub::DoubleBuffer<unsigned long long> kb(d_keys, d_keys2);
-        need = 0;
-        GB_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, need, kb, (int)refs, 0, 32 + cell_bits, st));
-        if (need > tmp_bytes) {
-            GB_TRY(B.alloc(&d_tmp, need));
-            tmp_bytes = need;
-        }
-        GB_TRY(hipcub::DeviceRadixSort::SortKeys(d_tmp, need, kb, (int)refs, 0, 32 + cell_bits, st));
-        hipLaunchKernelGGL(key_tri_kernel, dim3(blocks_for(refs)), dim3(kB), 0, st, kb.Current(), refs, d_idx);
+        uint32_t* d_rtmp;
+        GB_TRY(B.alloc(&d_rtmp, radix_tmp_items(refs)));
+        unsigned long long* sorted = nullptr;
+        GB_TRY(radix_sort(d_keys, d_keys2, refs, 32 + cell_bits, d_rtmp, st, &sorted));
+        hipLaunchKernelGGL(key_tri_kernel, dim3(blocks_for(refs)), dim3(kB), 0, st, (const unsigned long long*)sorted,
+                           refs, d_idx);
         GB_TRY(hipGetLastError());
     }
     uint2* d_cells;
@@ -346,8 +516,8 @@ int build_on_device(const float* positions, const float* normals, const float* t
 
 }  // namespace
 
-// Load this translation unit's code objects (its own module: the scans and
-// sorts) on the current device; called by zrt_device_warmup.
+// Load this translation unit's code objects on the current device; called
+// by zrt_device_warmup.
 int grid_build_warmup() {
     hipFuncAttributes fa;
     return hipFuncGetAttributes(&fa, (const void*)cand_kernel) == hipSuccess ? ZRT_OK : ZRT_ERR_HIP;
