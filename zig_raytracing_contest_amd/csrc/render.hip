@@ -613,9 +613,11 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 //    `nearest > t and t > 0` loop keeps (stage3.zig:164-178: the smallest t,
 //    the first ref among equal t; t > 0 orders like its bit pattern) -- and
 //    walks on from that cell;
-//  * finished lanes wait until `refill_min` of them are done, then shade
-//    together (traceRayRecursive's body, stage3.zig:195-219), append, and
-//    take fresh paths (persistent waves, dynamic fetch).
+//  * finished lanes wait until `refill_min` of them are done, then write
+//    their hit records (t, u, v, ref) together and take fresh paths from the
+//    wave's chunk of the queue (persistent waves, dynamic fetch);
+//    wf_shade_kernel then shades the hit records with whole waves
+//    (traceRayRecursive's body, stage3.zig:195-219) and appends.
 // Per lane the cells, the tests, their order semantics and the break test
 // after every cell (stage3.zig:179-182) are the reference's: same hit.
 //
@@ -1696,7 +1698,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // per-item bytes of a pass: counting megakernel = the float4 sample
     // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per
     // bounce slot
-    // (+ the 16 B hit record of the split park launches)
+    // (+ the 16 B hit record the park kernel hands the shade kernel)
     const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
     const uint64_t s_pass = pass_samples(cfg, per_item, P);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
