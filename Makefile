@@ -52,6 +52,13 @@ $(SWEEP_LIB): $(SRC)/render.hip $(HDRS) $(filter-out $(OBJ)/render.o,$(HIP_OBJS)
 	$(HIPCC) $(HIPFLAGS) -DZRT_SWEEP -c $(SRC)/render.hip -o tools/bin/sweep/render.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ tools/bin/sweep/render.o $(filter-out $(OBJ)/render.o,$(HIP_OBJS)) $(HOST_OBJS) -lz -pthread
 
+# A/B build of render.hip with extra defines (tools/gpu_ab.sh):
+#   make variant V=name D="-DZRT_FOO"  ->  tools/bin/name/libzrt.so
+variant: $(filter-out $(OBJ)/render.o,$(HIP_OBJS)) $(HOST_OBJS)
+	@mkdir -p tools/bin/$(V)
+	$(HIPCC) $(HIPFLAGS) $(D) -c $(SRC)/render.hip -o tools/bin/$(V)/render.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o tools/bin/$(V)/libzrt.so tools/bin/$(V)/render.o $^ -lz -pthread
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -59,4 +66,4 @@ clean:
 	rm -rf build $(LIB) $(PKG)/bin tools/bin
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all clean oracle sweep
+.PHONY: all clean oracle sweep variant

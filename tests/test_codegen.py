@@ -94,3 +94,45 @@ def test_park_kernel_m0_only_feeds_the_range_dma(code):
                 assert t.startswith(("s_mov_b32 m0,", "s_add_u32 m0, m0, 0x100")), (n, t)
             if t.startswith("global_load_lds"):
                 assert any(re.search(r"\bm0\b", x) for x in ins[max(0, i - 3):i]), (n, i, ins[i - 3:i + 1])
+
+
+def _loops(ins):
+    """(first index, last index) of every backward-branch loop body."""
+    import re
+    idx = {a: k for k, (a, _) in enumerate(ins)}
+    out = []
+    for k, (a, t) in enumerate(ins):
+        m = re.search(r"\bs_(?:cbranch_\w+|branch) (\d+)", t)
+        if not m:
+            continue
+        off = int(m.group(1))
+        off = off - 65536 if off > 32767 else off
+        tgt = a + 4 + 4 * off
+        if tgt <= a and tgt in idx:
+            out.append((idx[tgt], k))
+    return out
+
+
+def test_park_walk_trip_is_not_a_register_shuffle(code):
+    """The walk trip (two DDA steps, two OccX lookups = 4 LDS reads, one range
+    DMA issue point) stays ~145 VALU.  Its old branchy form let the compiler
+    copy the whole walk state through every join: a one-line change elsewhere
+    in the kernel took it from 160 to 232 VALU (96 v_mov) and cfg3 lost 2-3%
+    with identical images."""
+    sc, ks = code
+    ins = _kernel(ks, "wf_park_kernel")
+    trips = []
+    for b, e in _loops(ins):
+        body = [t.strip() for _, t in ins[b:e + 1]]
+        if sum(t.startswith("ds_read") for t in body) == 4 and not any(t.startswith("ds_write") for t in body) \
+                and any(t.startswith("global_load_lds") for t in ins_after(ins, e)):
+            trips.append(body)
+    assert trips, "walk loop not found"
+    body = min(trips, key=len)
+    valu = sum(t.startswith("v_") for t in body)
+    movs = sum(t.startswith("v_mov") for t in body)
+    assert valu <= 170 and movs <= 40, (valu, movs)
+
+
+def ins_after(ins, e, n=12):
+    return [t.strip() for _, t in ins[e + 1:e + 1 + n]]

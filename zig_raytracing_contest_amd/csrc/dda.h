@@ -149,6 +149,22 @@ ZHD void ddaw_from(const Dda& d, const GridK& g, DdaW& w) {
         (T_EXIT) = cc_ == ec_ ? kInf : tc_;                                          \
     } while (0)
 
+// Field-wise select of a walk state (a struct-level `c ? a : b` may become a
+// load through a selected pointer, see DDA_STEP).  Fields that are equal in
+// A and B (the per-axis constants) fold away.
+#define DDAW_SEL(D, C, A, B)                                                          \
+    do {                                                                             \
+        (D).tn0 = (C) ? (A).tn0 : (B).tn0; (D).tn1 = (C) ? (A).tn1 : (B).tn1;        \
+        (D).tn2 = (C) ? (A).tn2 : (B).tn2; (D).td0 = (C) ? (A).td0 : (B).td0;        \
+        (D).td1 = (C) ? (A).td1 : (B).td1; (D).td2 = (C) ? (A).td2 : (B).td2;        \
+        (D).c0 = (C) ? (A).c0 : (B).c0; (D).c1 = (C) ? (A).c1 : (B).c1;              \
+        (D).c2 = (C) ? (A).c2 : (B).c2; (D).lin = (C) ? (A).lin : (B).lin;           \
+        (D).e0 = (C) ? (A).e0 : (B).e0; (D).e1 = (C) ? (A).e1 : (B).e1;              \
+        (D).e2 = (C) ? (A).e2 : (B).e2; (D).s0 = (C) ? (A).s0 : (B).s0;              \
+        (D).s1 = (C) ? (A).s1 : (B).s1; (D).s2 = (C) ? (A).s2 : (B).s2;              \
+        (D).l1 = (C) ? (A).l1 : (B).l1; (D).l2 = (C) ? (A).l2 : (B).l2;              \
+    } while (0)
+
 // Empty-brick skip, 4^3 bricks (occ_shift 2): the state Iterator.next would
 // reach at the step that leaves the current brick, computed at once.  Axis
 // a's crossings form the sequence T_a(1) = tn_a, T_a(j+1) = T_a(j) + td_a

@@ -731,7 +731,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -797,6 +797,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
+            PARK_STAMP(10);
             // idle lanes take entries of the wave's chunk [cb, ce) of group
             // cgrp, a new chunk of kParkChunk entries once it is used up: one
             // returning atomic per chunk instead of one per refill round
@@ -805,6 +806,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 if (cb == ce) {
                     uint32_t base = 0, lim = 0;
                     more = wf_fetch<false>(w, kParkChunk, grp, tried, base, lim);
+                    PARK_STAMP(11);
                     if (!more) break;
                     cb = base;
                     ce = min(base + kParkChunk, lim);
@@ -840,6 +842,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                         }
                     }
                 }
+                PARK_STAMP(12);
                 cb += take;
                 idle = __ballot(st == kIdle);
             }
@@ -869,26 +872,23 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 DDAW_STEP(s2, 2u, cr2, te2);
                 unsigned long long q1 = occx_mask_clamped(L, occx_brick(w, s1), w.occx_nbw);
                 unsigned long long q2 = occx_mask_clamped(L, occx_brick(w, s2), w.occx_nbw);
-                // both lookups complete here, ahead of the branches below
+                // both lookups complete here, ahead of the selects below
                 // (left alone, the compiler sinks the second into the branch
                 // that uses it and the two LDS chains run one after the other)
                 asm volatile("" : "+v"(q1), "+v"(q2));
                 const unsigned long long m1 = cr1 ? q1 : bm;
                 const unsigned long long m2 = cr2 ? q2 : m1;
-                bool pk = false;
-                if (nearest <= te1) {                              // stage3.zig:179-182
-                    st = kDone;
-                } else if (occx_cell(m1, s1)) {
-                    s = s1;
-                    bm = m1;
-                    pk = true;
-                } else if (nearest <= te2) {
-                    st = kDone;
-                } else {
-                    s = s2;
-                    bm = m2;
-                    pk = occx_cell(m2, s2);
-                }
+                // the trip ends in the first of its cells that ends the
+                // segment (stage3.zig:179-182) or holds triangles; selects,
+                // not branches: the branchy form made the compiler copy the
+                // whole state through every join (up to 232 VALU per trip)
+                const bool d1 = nearest <= te1, d2 = nearest <= te2;
+                const bool o1 = occx_cell(m1, s1), o2 = occx_cell(m2, s2);
+                const bool at1 = d1 || o1;
+                const bool pk = at1 ? !d1 : (!d2 && o2);
+                if (at1 ? d1 : d2) st = kDone;
+                DDAW_SEL(s, at1, s1, s2);
+                bm = at1 ? m1 : m2;
                 if (pk) {                                          // one issue point per trip
                     park_load_range(p, s.lin, rng_slot);
                     st = kPark;
@@ -956,7 +956,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
 #ifdef ZRT_SWEEP
     if (lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
+        for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
 #endif
 }
 
@@ -1887,8 +1887,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_park_profile\": {\"cyc_shade_refill\": %llu, \"cyc_walk\": %llu, \"cyc_test\": %llu, "
                 "\"walk_iters\": %llu, \"walk_lanes\": %llu, \"test_rounds\": %llu, \"sub_rounds\": %llu, "
-                "\"pairs\": %llu, \"refill_rounds\": %llu, \"shaded_lanes\": %llu}}\n",
-                hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25]);
+                "\"pairs\": %llu, \"refill_rounds\": %llu, \"shaded_lanes\": %llu, \"cyc_drain\": %llu, "
+                "\"cyc_atomic\": %llu, \"cyc_setup\": %llu}}\n",
+                hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
 #endif
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
