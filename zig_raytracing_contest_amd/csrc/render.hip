@@ -1749,6 +1749,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 #endif
     const uint32_t occx_ldsw = (uint32_t)occx_lds_words(c->occx_nbw, c->occx_moff, c->occx_words);
     const size_t lds_park = 4ull * occx_ldsw + (size_t)(park_block / 64) * sizeof(ParkSlot);
+    if (getenv("ZRT_WF_DEBUG"))
+        fprintf(stderr, "{\"zrt_park_lds\": {\"occx_bytes\": %u, \"block\": %d, \"lds_per_block\": %zu}}\n",
+                4u * occx_ldsw, park_block, lds_park);
     auto grid_for = [&](const void* f, int threads, size_t lds, uint32_t* blocks) -> int {
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
