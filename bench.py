@@ -287,10 +287,11 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    kern_ms, launches, segs = 0.0, 0, 0
+    kern_ms, gpu_ms, launches, segs = 0.0, 0.0, 0, 0
     for _ in range(a.steps):
         st = step()
         kern_ms += st["trace_kernel_ms"]
+        gpu_ms += st["render_ms"]
         launches += st["trace_launches"]
         segs += st["segments"]
     barrier()
@@ -306,11 +307,17 @@ def main():
 
     if rank == 0:
         assert cst["segments"] * a.steps == segs, "counting and timed kernels disagree"
-        avg_launch_s = kern_ms / 1e3 / max(launches, 1)
+        # two passes are in flight at once on two HIP streams (DESIGN.md
+        # §5), so launches overlap: a launch's share of the machine is the
+        # step's GPU time (HIP events from the first launch to the join of
+        # both streams) over its launches, and achieved = the step's
+        # algorithmic bytes over that GPU time.  The per-launch event
+        # intervals (what rocprofv3 reports as kernel durations, overlapped)
+        # are kept beside it.
+        avg_launch_s = gpu_ms / 1e3 / max(launches, 1)
+        overlapped_launch_s = kern_ms / 1e3 / max(launches, 1)
         alg_bytes = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] +
                      B_HIT * cst["hits"] + B_PIX * P)
-        # bytes per timed launch = the step's bytes / the step's launches, so
-        # achieved = sum(bytes) / sum(launch durations) over the step
         per_launch = alg_bytes / max(launches / a.steps, 1)
         achieved = per_launch / avg_launch_s / 1e9
         out = {
@@ -338,6 +345,11 @@ def main():
                          "kernel": "trace launches: wf_kernel<7,true> (primary), wf_park_kernel + "
                                    "wf_shade_kernel (each bounce)",
                          "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "avg_launch_ms_overlapped": round(overlapped_launch_s * 1e3, 3),
+                         "gpu_ms_per_step": round(gpu_ms / a.steps, 3),
+                         "launch_time": "step GPU time / launches: two passes run at once on two "
+                                        "HIP streams, so launches overlap; avg_launch_ms_overlapped "
+                                        "is the per-launch HIP-event interval (rocprofv3's durations)",
                          "alg_GB_per_launch": round(per_launch / 1e9, 3)},
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},

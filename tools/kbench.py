@@ -2,6 +2,7 @@
 """Variant sweep on one GPU: same frame, several env settings, one process.
 Checks every variant's image is identical to the first (exactness guard)."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -37,15 +38,16 @@ if a.cell_stats:
 for var in (a.var or [""]):
     env = dict(kv.split("=") for kv in var.split(",") if kv)
     flags = int(env.pop("FLAGS", "0"), 0)   # zrt_render_config.flags (ZRT_FLAG_*)
+    spp_pass = int(env.pop("SPP_PASS", "0"))  # zrt_render_config.samples_per_pass (0 = auto)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     ctx = native.Context(geo.scene)
     img = np.zeros((cam.h, cam.w, 3), np.uint8)
-    ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags)   # warm
+    ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags, samples_per_pass=spp_pass)   # warm
     ts = []
     for _ in range(a.reps):
         t0 = time.perf_counter()
-        r = ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags)
+        r = ctx.render(cam, a.spp, cfg["max_bounce"], image=img, flags=flags, samples_per_pass=spp_pass)
         ts.append(time.perf_counter() - t0)
     st = r["stats"]
     same = True if ref is None else bool(np.array_equal(ref, img))
@@ -53,7 +55,8 @@ for var in (a.var or [""]):
         ref = img.copy()
     rec = {"var": var or "default", "mrays": round(st["segments"] / min(ts) / 1e6, 1),
            "kernel_ms": round(st["trace_kernel_ms"], 2), "wall_ms": round(min(ts) * 1e3, 2),
-           "identical": same, "segments": int(st["segments"])}
+           "identical": same, "segments": int(st["segments"]),
+           "img_sha1": hashlib.sha1(img.tobytes()).hexdigest()[:12]}
     if not same:
         dif = np.any(ref != img, axis=2)
         rec["diff_pixels"] = int(dif.sum())

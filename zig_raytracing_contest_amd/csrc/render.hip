@@ -1162,6 +1162,16 @@ struct zrt_context {
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
     float* d_lin = nullptr; size_t lin_cap = 0;
+    // the second pass set: odd passes run on stream2 with their own queues
+    hipStream_t stream2 = nullptr;
+    float4* d_q0b = nullptr; size_t q0b_cap = 0;
+    float4* d_q1b = nullptr; size_t q1b_cap = 0;
+    float4* d_termb = nullptr; size_t termb_cap = 0;
+    float4* d_stkb = nullptr; size_t stkb_cap = 0;
+    uint32_t* d_wfcb = nullptr; size_t wfcb_cap = 0;
+    float4* d_hitb = nullptr; size_t hitb_cap = 0;
+    std::vector<hipEvent_t> ev_pass;   // per pass: its resolve done
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint32_t* d_counter = nullptr;
     unsigned long long* d_stats = nullptr;
     int num_cus = 0;
@@ -1251,10 +1261,15 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     DeviceGuard g(c->device);
     void* bufs[] = {c->d_cells, c->d_pos,  c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ,
                     c->d_occx,  c->d_pix,  c->d_out,  c->d_q0,   c->d_q1,     c->d_term, c->d_stk,
-                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats, c->d_hit};
+                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats, c->d_hit,
+                    c->d_q0b,   c->d_q1b,  c->d_termb, c->d_stkb, c->d_wfcb, c->d_hitb};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_pass) (void)hipEventDestroy(e);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
     if (c->ev_end) (void)hipEventDestroy(c->ev_end);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1645,17 +1660,25 @@ extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t in
 // Samples per pass: the caller's cfg->samples_per_pass, else as many as fit
 // a 40 GiB budget of queues + bounce planes (HBM is 288 GB; cfg3 then runs 3
 // passes of <= 86 spp) and 60% of the free device memory.
-static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P) {
+// Samples per pass.  Two pass sets run on two streams (the kernels of one
+// pass overlap the other's), so by default a frame has at least two passes,
+// as few as the queue budget allows, split evenly: cfg3 256 spp = 2 x 128
+// (r02bq, two streams: 2 x 128 265.5 ms, 4 x 64 269.2, 8 x 32 273.1; cfg2
+// 64 spp: 2 x 32 18.1 ms vs one pass 20.1).  The budget is for both sets:
+// 144 GiB, at most 60% of the free HBM.
+static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P, uint32_t sets) {
+    const uint64_t spp = cfg->num_samples;
     uint64_t s_pass;
     if (cfg->samples_per_pass) {
-        s_pass = cfg->samples_per_pass;
+        s_pass = std::min<uint64_t>(cfg->samples_per_pass, spp);
     } else {
-        size_t budget = (size_t)40 << 30;
+        size_t budget = (size_t)144 << 30;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) budget = std::min(budget, free_b / 10 * 6);
-        s_pass = std::max<uint64_t>(1, budget / (per_item * P));
+        const uint64_t fit = std::max<uint64_t>(1, budget / sets / (per_item * P));
+        const uint64_t npass = std::max<uint64_t>(std::min<uint64_t>(sets, spp), (spp + fit - 1) / fit);
+        s_pass = (spp + npass - 1) / npass;
     }
-    s_pass = std::min<uint64_t>(s_pass, cfg->num_samples);
     return std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
 }
 
@@ -1700,7 +1723,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // bounce slot
     // (+ the 16 B hit record the park kernel hands the shade kernel)
     const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
-    const uint64_t s_pass = pass_samples(cfg, per_item, P);
+    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : 2u);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     const uint64_t T = s_pass * P;
     int rc;
@@ -1712,6 +1735,26 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&c->d_wfc, &c->wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
     } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
         return rc;
+    }
+    // two pass sets: odd passes on stream2 with their own queues, so that
+    // one pass's launches fill the machine while the other's drain (tails,
+    // the latency-bound shade kernel beside the park kernel): cfg3 -6%, cfg5
+    // -8% frame time, images identical (r02bp)
+    const uint32_t nsets = (!counting && npasses > 1) ? 2u : 1u;
+    if (nsets == 2) {
+        if ((rc = grow(&c->d_q0b, &c->q0b_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_q1b, &c->q1b_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_termb, &c->termb_cap, T)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_stkb, &c->stkb_cap, 2 * T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&c->d_wfcb, &c->wfcb_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
+        if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        while (c->ev_pass.size() < npasses) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->ev_pass.push_back(e);
+        }
     }
     if (npasses > 1 && (rc = grow(&c->d_acc, &c->acc_cap, P)) != ZRT_OK) return rc;
     if ((rc = grow(&c->d_rgb, &c->rgb_cap, 3ull * P)) != ZRT_OK) return rc;
@@ -1740,6 +1783,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : kWfBounce;
     const WfFn s_next = (WfFn)wf_shade_kernel;
     if (park_next && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
+    if (park_next && nsets == 2 && (rc = grow(&c->d_hitb, &c->hitb_cap, T)) != ZRT_OK) return rc;
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
@@ -1808,8 +1852,22 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
+    if (nsets == 2) {                          // stream2 starts after the stats reset
+        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    }
     uint32_t launches = 0, ne = 0;
     for (uint32_t pass = 0; pass < npasses; ++pass) {
+        // pass set: even passes on the context stream, odd ones on stream2
+        // with their own queues, so one pass's kernels overlap the other's
+        const bool sb = nsets == 2 && (pass & 1u);
+        hipStream_t sm = sb ? c->stream2 : c->stream;
+        float4* const q0 = sb ? c->d_q0b : c->d_q0;
+        float4* const q1 = sb ? c->d_q1b : c->d_q1;
+        float4* const term = sb ? c->d_termb : c->d_term;
+        float4* const stk = sb ? c->d_stkb : c->d_stk;
+        uint32_t* const wfc = sb ? c->d_wfcb : c->d_wfc;
+        float4* const hit = sb ? c->d_hitb : c->d_hit;
         const uint32_t s0 = (uint32_t)(pass * s_pass);
         const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
         tp.s0 = s0;
@@ -1818,12 +1876,12 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if (!counting) {
             // per launch k: 8 work counters, then 8 region counts of the
             // paths entering launch k (written by launch k - 1)
-            HIP_TRY(hipMemsetAsync(c->d_wfc, 0, 4ull * 24 * kCtr * (mb + 2), c->stream));
+            HIP_TRY(hipMemsetAsync(wfc, 0, 4ull * 24 * kCtr * (mb + 2), sm));
             WfParams W;
             memset(&W, 0, sizeof W);
             W.t = tp;
-            W.stk = c->d_stk;
-            W.term = c->d_term;
+            W.stk = stk;
+            W.term = term;
             W.T = (uint32_t)T;
             W.occx = c->d_occx;
             W.occx_words = c->occx_words;
@@ -1835,29 +1893,32 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.test_min = test_min;
             W.refill_min = refill_min;
             for (uint32_t k = 0; k < nb; ++k) {
-                W.q_in = (k & 1) ? c->d_q0 : c->d_q1;
-                W.q_out = (k & 1) ? c->d_q1 : c->d_q0;
-                W.fetch8 = c->d_wfc + kCtr * (16 * k);
-                W.n_in8 = c->d_wfc + kCtr * (16 * k + 8);
-                W.n_out8 = c->d_wfc + kCtr * (16 * (k + 1) + 8);
-                W.hit = c->d_hit;
-                W.fetch8s = c->d_wfc + kCtr * (16 * (mb + 2) + 8 * k);
-                HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                W.q_in = (k & 1) ? q0 : q1;
+                W.q_out = (k & 1) ? q1 : q0;
+                W.fetch8 = wfc + kCtr * (16 * k);
+                W.n_in8 = wfc + kCtr * (16 * k + 8);
+                W.n_out8 = wfc + kCtr * (16 * (k + 1) + 8);
+                W.hit = hit;
+                W.fetch8s = wfc + kCtr * (16 * (mb + 2) + 8 * k);
+                HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 if (k == 0)
-                    hipLaunchKernelGGL(f_first, dim3(grid_first), dim3(thr_first), lds_first, c->stream, W);
+                    hipLaunchKernelGGL(f_first, dim3(grid_first), dim3(thr_first), lds_first, sm, W);
                 else
-                    hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, c->stream, W);
+                    hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, sm, W);
                 HIP_TRY(hipGetLastError());
                 if (k > 0 && park_next) {                    // same bounce, shading half
-                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), 0, c->stream, W);
+                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), 0, sm, W);
                     HIP_TRY(hipGetLastError());
                 }
-                HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+                HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 ++launches;
             }
-            hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
-                               c->d_term, c->d_stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
+            // the passes' sums into acc stay in pass order (stage3.zig:236-242)
+            if (nsets == 2 && pass > 0) HIP_TRY(hipStreamWaitEvent(sm, c->ev_pass[pass - 1], 0));
+            hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, sm,
+                               term, stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
                                c->d_rgb, want_lin ? c->d_lin : nullptr);
+            if (nsets == 2) HIP_TRY(hipEventRecord(c->ev_pass[pass], sm));
         } else {
             HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
@@ -1870,6 +1931,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                                want_lin ? c->d_lin : nullptr);
         }
         HIP_TRY(hipGetLastError());
+    }
+    if (nsets == 2) {                          // join: stream2's passes are done
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     }
     HIP_TRY(hipEventRecord(c->ev_end, c->stream));
     if (outs && outs->device_rgb_packed)
