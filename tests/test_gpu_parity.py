@@ -331,7 +331,9 @@ sys.path[:0] = [os.environ["ZRT_ROOT"], os.path.join(os.environ["ZRT_ROOT"], "or
 from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
 import oracle as orc
 out = {}
+extra = int(os.environ.get("ZRT_TEST_EXTRA_SPP", "0"))
 for name, cam_name, h, spp in (("contest", "Camera 1", 54, 2), ("sponza", None, 40, 2), ("sphere", None, 40, 3)):
+    spp += extra
     soup = scenes.get_scene(name)
     c = soup.camera(cam_name)
     cam = camera_for(soup, cam_name, None if c.aspect else h, h)
@@ -358,6 +360,26 @@ def test_park_schedule_extremes_bitexact(t, r):
     if not os.path.exists(lib):
         pytest.fail("tools/bin/sweep/libzrt.so not built (make)")
     env = dict(os.environ, ZRT_LIB=lib, ZRT_ROOT=root, ZRT_PARK_T=str(t), ZRT_PARK_R=str(r))
+    p = subprocess.run([sys.executable, "-c", _SCHEDULE_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert all(res.values()), res
+
+
+@pytest.mark.parametrize("sets", [1, 3, 4])
+def test_pass_sets_bitexact(sets):
+    """1, 3 or 4 pass sets in flight (one HIP stream and one set of queues
+    each; the product runs 2): every frame renders bit-exact vs the oracle
+    (-DZRT_SWEEP build reads ZRT_SETS; 4-6 spp so every set gets a pass)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "tools", "bin", "sweep", "libzrt.so")
+    if not os.path.exists(lib):
+        pytest.fail("tools/bin/sweep/libzrt.so not built (make)")
+    env = dict(os.environ, ZRT_LIB=lib, ZRT_ROOT=root, ZRT_SETS=str(sets), ZRT_TEST_EXTRA_SPP="3")
     p = subprocess.run([sys.executable, "-c", _SCHEDULE_SCRIPT], env=env, capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]

@@ -1127,6 +1127,9 @@ int grow(T** p, size_t* cap, size_t n) {
 // OccX (wf_park_kernel): LDS left for the blob in one 1024-thread workgroup
 // per CU after the per-wave ParkSlots and the static ziggurat tables.
 constexpr size_t kLdsPerCu = 160 * 1024;
+// pass sets in flight (streams) by default, and at most (ZRT_SWEEP: ZRT_SETS)
+constexpr uint32_t kPassSets = 2;
+constexpr uint32_t kMaxPassSets = 4;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 128 * 4 - 256;
 
@@ -1153,25 +1156,24 @@ struct zrt_context {
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;     // counting build
-    float4* d_q0 = nullptr; size_t q0_cap = 0;       // wavefront queues
-    float4* d_q1 = nullptr; size_t q1_cap = 0;
-    float4* d_term = nullptr; size_t term_cap = 0;
-    float4* d_stk = nullptr; size_t stk_cap = 0;
-    uint32_t* d_wfc = nullptr; size_t wfc_cap = 0;
-    float4* d_hit = nullptr; size_t hit_cap = 0;     // split park launches: hit records
+    // wavefront buffers of one pass set (queues, terminal radiance, bounce
+    // planes, counters, hit records); set k > 0 runs on its own stream
+    struct PassSet {
+        hipStream_t stream = nullptr;      // set 0: the context stream
+        float4* q0 = nullptr; size_t q0_cap = 0;
+        float4* q1 = nullptr; size_t q1_cap = 0;
+        float4* term = nullptr; size_t term_cap = 0;
+        float4* stk = nullptr; size_t stk_cap = 0;
+        uint32_t* wfc = nullptr; size_t wfc_cap = 0;
+        float4* hit = nullptr; size_t hit_cap = 0;
+        hipEvent_t ev_join = nullptr;      // set k > 0: its last pass is done
+    };
+    PassSet set[kMaxPassSets];
     float4* d_acc = nullptr; size_t acc_cap = 0;
     uint8_t* d_rgb = nullptr; size_t rgb_cap = 0;
     float* d_lin = nullptr; size_t lin_cap = 0;
-    // the second pass set: odd passes run on stream2 with their own queues
-    hipStream_t stream2 = nullptr;
-    float4* d_q0b = nullptr; size_t q0b_cap = 0;
-    float4* d_q1b = nullptr; size_t q1b_cap = 0;
-    float4* d_termb = nullptr; size_t termb_cap = 0;
-    float4* d_stkb = nullptr; size_t stkb_cap = 0;
-    uint32_t* d_wfcb = nullptr; size_t wfcb_cap = 0;
-    float4* d_hitb = nullptr; size_t hitb_cap = 0;
     std::vector<hipEvent_t> ev_pass;   // per pass: its resolve done
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr;
     uint32_t* d_counter = nullptr;
     unsigned long long* d_stats = nullptr;
     int num_cus = 0;
@@ -1259,17 +1261,20 @@ extern "C" int zrt_device_warmup(int device) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    void* bufs[] = {c->d_cells, c->d_pos,  c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ,
-                    c->d_occx,  c->d_pix,  c->d_out,  c->d_q0,   c->d_q1,     c->d_term, c->d_stk,
-                    c->d_wfc,   c->d_acc,  c->d_rgb,  c->d_lin,  c->d_counter, c->d_stats, c->d_hit,
-                    c->d_q0b,   c->d_q1b,  c->d_termb, c->d_stkb, c->d_wfcb, c->d_hitb};
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
+                    c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (zrt_context::PassSet& ps : c->set) {
+        void* sb[] = {ps.q0, ps.q1, ps.term, ps.stk, ps.wfc, ps.hit};
+        for (void* b : sb)
+            if (b) (void)hipFree(b);
+        if (ps.ev_join) (void)hipEventDestroy(ps.ev_join);
+        if (ps.stream && ps.stream != c->stream) (void)hipStreamDestroy(ps.stream);
+    }
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_pass) (void)hipEventDestroy(e);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
     if (c->ev_end) (void)hipEventDestroy(c->ev_end);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1657,15 +1662,12 @@ extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t in
     return ZRT_OK;
 }
 
-// Samples per pass: the caller's cfg->samples_per_pass, else as many as fit
-// a 40 GiB budget of queues + bounce planes (HBM is 288 GB; cfg3 then runs 3
-// passes of <= 86 spp) and 60% of the free device memory.
-// Samples per pass.  Two pass sets run on two streams (the kernels of one
-// pass overlap the other's), so by default a frame has at least two passes,
-// as few as the queue budget allows, split evenly: cfg3 256 spp = 2 x 128
-// (r02bq, two streams: 2 x 128 265.5 ms, 4 x 64 269.2, 8 x 32 273.1; cfg2
-// 64 spp: 2 x 32 18.1 ms vs one pass 20.1).  The budget is for both sets:
-// 144 GiB, at most 60% of the free HBM.
+// Samples per pass: the caller's cfg->samples_per_pass, else as few passes
+// as the queue budget allows but at least one per pass set (the sets' kernels
+// overlap on their streams), split evenly: cfg3 256 spp = 2 x 128 (r02bq, two
+// streams: 2 x 128 265.5 ms, 4 x 64 269.2, 8 x 32 273.1; cfg2 64 spp: 2 x 32
+// 18.1 ms vs one pass 20.1).  The budget covers every set: 144 GiB (HBM is
+// 288 GB), at most 60% of the free device memory.
 static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P, uint32_t sets) {
     const uint64_t spp = cfg->num_samples;
     uint64_t s_pass;
@@ -1723,33 +1725,36 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // bounce slot
     // (+ the 16 B hit record the park kernel hands the shade kernel)
     const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
-    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : 2u);
+    uint32_t want_sets = kPassSets;
+#if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
+    if (const char* e = getenv("ZRT_SETS")) want_sets = (uint32_t)std::max(1, std::min((int)kMaxPassSets, atoi(e)));
+#endif
+    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     const uint64_t T = s_pass * P;
     int rc;
-    if (!counting) {
-        if ((rc = grow(&c->d_q0, &c->q0_cap, 3 * T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_q1, &c->q1_cap, 3 * T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_term, &c->term_cap, T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_stk, &c->stk_cap, 2 * T * nb)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfc, &c->wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
-    } else if ((rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) {
-        return rc;
+    // pass sets: pass p runs on set p % nsets, each set with its own stream
+    // and buffers, so one pass's launches fill the machine while another's
+    // drain (tails, the latency-bound shade kernel beside the park kernel):
+    // two sets cfg3 -5%, cfg2 -9%, cfg5 -7% frame time, images identical
+    // (r02c1, profiles/r02/r02c1_ab_two_streams.log)
+    const uint32_t nsets = counting ? 1u : std::min<uint32_t>(npasses, want_sets);
+    for (uint32_t k = 0; k < nsets && !counting; ++k) {
+        zrt_context::PassSet& ps = c->set[k];
+        if ((rc = grow(&ps.q0, &ps.q0_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.q1, &ps.q1_cap, 3 * T)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.term, &ps.term_cap, T)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.stk, &ps.stk_cap, 2 * T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.wfc, &ps.wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
+        if (k == 0) {
+            ps.stream = c->stream;
+        } else {
+            if (!ps.stream) HIP_TRY(hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking));
+            if (!ps.ev_join) HIP_TRY(hipEventCreateWithFlags(&ps.ev_join, hipEventDisableTiming));
+        }
     }
-    // two pass sets: odd passes on stream2 with their own queues, so that
-    // one pass's launches fill the machine while the other's drain (tails,
-    // the latency-bound shade kernel beside the park kernel): cfg3 -6%, cfg5
-    // -8% frame time, images identical (r02bp)
-    const uint32_t nsets = (!counting && npasses > 1) ? 2u : 1u;
-    if (nsets == 2) {
-        if ((rc = grow(&c->d_q0b, &c->q0b_cap, 3 * T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_q1b, &c->q1b_cap, 3 * T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_termb, &c->termb_cap, T)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_stkb, &c->stkb_cap, 2 * T * nb)) != ZRT_OK) return rc;
-        if ((rc = grow(&c->d_wfcb, &c->wfcb_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
-        if (!c->stream2) HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    if (nsets > 1) {
         if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
         while (c->ev_pass.size() < npasses) {
             hipEvent_t e;
             HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1782,8 +1787,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const WfFn f_first = kWfPrimary;
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : kWfBounce;
     const WfFn s_next = (WfFn)wf_shade_kernel;
-    if (park_next && (rc = grow(&c->d_hit, &c->hit_cap, T)) != ZRT_OK) return rc;
-    if (park_next && nsets == 2 && (rc = grow(&c->d_hitb, &c->hitb_cap, T)) != ZRT_OK) return rc;
+    for (uint32_t k = 0; k < nsets && park_next; ++k)
+        if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
@@ -1852,22 +1857,21 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
-    if (nsets == 2) {                          // stream2 starts after the stats reset
+    if (nsets > 1) {                           // the other sets start after the stats reset
         HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+        for (uint32_t k = 1; k < nsets; ++k) HIP_TRY(hipStreamWaitEvent(c->set[k].stream, c->ev_fork, 0));
     }
     uint32_t launches = 0, ne = 0;
     for (uint32_t pass = 0; pass < npasses; ++pass) {
-        // pass set: even passes on the context stream, odd ones on stream2
-        // with their own queues, so one pass's kernels overlap the other's
-        const bool sb = nsets == 2 && (pass & 1u);
-        hipStream_t sm = sb ? c->stream2 : c->stream;
-        float4* const q0 = sb ? c->d_q0b : c->d_q0;
-        float4* const q1 = sb ? c->d_q1b : c->d_q1;
-        float4* const term = sb ? c->d_termb : c->d_term;
-        float4* const stk = sb ? c->d_stkb : c->d_stk;
-        uint32_t* const wfc = sb ? c->d_wfcb : c->d_wfc;
-        float4* const hit = sb ? c->d_hitb : c->d_hit;
+        // pass set pass % nsets: its own stream and buffers
+        const zrt_context::PassSet& ps = c->set[counting ? 0u : pass % nsets];
+        hipStream_t sm = counting ? c->stream : ps.stream;
+        float4* const q0 = ps.q0;
+        float4* const q1 = ps.q1;
+        float4* const term = ps.term;
+        float4* const stk = ps.stk;
+        uint32_t* const wfc = ps.wfc;
+        float4* const hit = ps.hit;
         const uint32_t s0 = (uint32_t)(pass * s_pass);
         const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
         tp.s0 = s0;
@@ -1914,11 +1918,11 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 ++launches;
             }
             // the passes' sums into acc stay in pass order (stage3.zig:236-242)
-            if (nsets == 2 && pass > 0) HIP_TRY(hipStreamWaitEvent(sm, c->ev_pass[pass - 1], 0));
+            if (nsets > 1 && pass > 0) HIP_TRY(hipStreamWaitEvent(sm, c->ev_pass[pass - 1], 0));
             hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, sm,
                                term, stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
                                c->d_rgb, want_lin ? c->d_lin : nullptr);
-            if (nsets == 2) HIP_TRY(hipEventRecord(c->ev_pass[pass], sm));
+            if (nsets > 1) HIP_TRY(hipEventRecord(c->ev_pass[pass], sm));
         } else {
             HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
@@ -1932,9 +1936,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         }
         HIP_TRY(hipGetLastError());
     }
-    if (nsets == 2) {                          // join: stream2's passes are done
-        HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    for (uint32_t k = 1; k < nsets; ++k) {     // join: the other sets' passes are done
+        HIP_TRY(hipEventRecord(c->set[k].ev_join, c->set[k].stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->set[k].ev_join, 0));
     }
     HIP_TRY(hipEventRecord(c->ev_end, c->stream));
     if (outs && outs->device_rgb_packed)
