@@ -1739,6 +1739,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // two sets cfg3 -5%, cfg2 -9%, cfg5 -7% frame time, images identical
     // (r02c1, profiles/r02/r02c1_ab_two_streams.log)
     const uint32_t nsets = counting ? 1u : std::min<uint32_t>(npasses, want_sets);
+    if (counting && (rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) return rc;
     for (uint32_t k = 0; k < nsets && !counting; ++k) {
         zrt_context::PassSet& ps = c->set[k];
         if ((rc = grow(&ps.q0, &ps.q0_cap, 3 * T)) != ZRT_OK) return rc;
