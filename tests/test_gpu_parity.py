@@ -274,23 +274,27 @@ def test_render_multipass_and_ranks_identical(gpu_scenes, mode, flags):
 
 
 def test_two_stream_pass_sets_identical(gpu_scenes):
-    """Passes alternate between two HIP streams with their own queues; the
-    passes' sums into the accumulator must stay in pass order: one pass, the
-    default split (two passes) and five one-sample passes give the same
-    image and the same linear radiance."""
+    """Passes alternate between two HIP streams with their own queues once a
+    frame has 2^23 samples; the passes' sums into the accumulator must stay in
+    pass order: one pass, the default split (two passes on two sets) and
+    eight passes give the same image and the same linear radiance.  A small
+    frame runs one pass on one set."""
     soup = scenes.get_scene("cornell")
-    cam = camera_for(soup, None, 72, 64)
+    cam = camera_for(soup, None, 512, 512)
     rs = gpu_scenes("cornell")
-    one, r1 = rs.render(cam, num_samples=5, max_bounce=4, samples_per_pass=5, linear=True)
+    one, r1 = rs.render(cam, num_samples=32, max_bounce=4, samples_per_pass=32, linear=True)
     assert r1["stats"]["trace_launches"] == 4
-    dflt, r2 = rs.render(cam, num_samples=5, max_bounce=4, linear=True)
-    assert r2["stats"]["trace_launches"] == 2 * 4          # default: at least two passes
-    five, r5 = rs.render(cam, num_samples=5, max_bounce=4, samples_per_pass=1, linear=True)
-    assert r5["stats"]["trace_launches"] == 5 * 4
-    for img, r in ((dflt, r2), (five, r5)):
+    dflt, r2 = rs.render(cam, num_samples=32, max_bounce=4, linear=True)
+    assert r2["stats"]["trace_launches"] == 2 * 4          # 2^23 samples: two sets, one pass each
+    eight, r8 = rs.render(cam, num_samples=32, max_bounce=4, samples_per_pass=4, linear=True)
+    assert r8["stats"]["trace_launches"] == 8 * 4
+    for img, r in ((dflt, r2), (eight, r8)):
         assert np.array_equal(one, img)
         assert np.array_equal(r1["linear"], r["linear"])
         assert r["stats"]["segments"] == r1["stats"]["segments"]
+    small = camera_for(soup, None, 72, 64)
+    _, rs5 = rs.render(small, num_samples=5, max_bounce=4)
+    assert rs5["stats"]["trace_launches"] == 4             # small frame: one pass
 
 
 @pytest.mark.parametrize("mode,flags", MODES + [("counting", 0)], ids=[m for m, _ in MODES] + ["counting"])

@@ -1130,6 +1130,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 // pass sets in flight (streams) by default, and at most (ZRT_SWEEP: ZRT_SETS)
 constexpr uint32_t kPassSets = 2;
 constexpr uint32_t kMaxPassSets = 4;
+constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that runs kPassSets
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 128 * 4 - 256;
 
@@ -1668,20 +1669,25 @@ extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t in
 // streams: 2 x 128 265.5 ms, 4 x 64 269.2, 8 x 32 273.1; cfg2 64 spp: 2 x 32
 // 18.1 ms vs one pass 20.1).  The budget covers every set: 144 GiB (HBM is
 // 288 GB), at most 60% of the free device memory.
-static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P, uint32_t sets) {
+// `held`: the bytes of pass buffers this context already holds (grow-only,
+// reused by this render), counted as free: otherwise the split would depend
+// on the renders before (a warm context saw less free memory and ran 3 passes
+// on 2 sets, the last one alone).  The pass count is a multiple of the sets
+// (when spp allows), so the streams stay balanced to the end of the frame.
+static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P, uint32_t sets,
+                             size_t held) {
     const uint64_t spp = cfg->num_samples;
-    uint64_t s_pass;
-    if (cfg->samples_per_pass) {
-        s_pass = std::min<uint64_t>(cfg->samples_per_pass, spp);
-    } else {
-        size_t budget = (size_t)144 << 30;
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) budget = std::min(budget, free_b / 10 * 6);
-        const uint64_t fit = std::max<uint64_t>(1, budget / sets / (per_item * P));
-        const uint64_t npass = std::max<uint64_t>(std::min<uint64_t>(sets, spp), (spp + fit - 1) / fit);
-        s_pass = (spp + npass - 1) / npass;
-    }
-    return std::min<uint64_t>(s_pass, std::max<uint64_t>(1, 0x7FFFFF00ull / P));
+    const uint64_t cap = std::max<uint64_t>(1, 0x7FFFFF00ull / P);     // items of a pass < 2^31
+    if (cfg->samples_per_pass) return std::min<uint64_t>(std::min<uint64_t>(cfg->samples_per_pass, spp), cap);
+    size_t budget = (size_t)144 << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+        budget = std::min(budget, (free_b + held) / 10 * 6);
+    const uint64_t fit = std::min<uint64_t>(cap, std::max<uint64_t>(1, budget / sets / (per_item * P)));
+    uint64_t npass = std::max<uint64_t>(std::min<uint64_t>(sets, spp), (spp + fit - 1) / fit);
+    npass = std::min<uint64_t>(spp, (npass + sets - 1) / sets * sets);
+    const uint64_t s_pass = (spp + npass - 1) / npass;
+    return s_pass;
 }
 
 extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const zrt_render_config* cfg,
@@ -1725,11 +1731,19 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // bounce slot
     // (+ the 16 B hit record the park kernel hands the shade kernel)
     const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
-    uint32_t want_sets = kPassSets;
+    // small frames run one set: a second stream costs its first launches
+    // (the zrt CLI's 3-spp 1080p frame rendered in 30-39 vs 12.5-13.3 ms on a
+    // fresh process) and does not pay back (cfg3 at 3 spp, warm: 7.1 vs 6.8
+    // ms), while cfg2 (16.8 M samples) gains 10% (r02c4)
+    const bool big = (uint64_t)P * cfg->num_samples >= kSetsMinSamples;
+    uint32_t want_sets = big ? kPassSets : 1u;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_SETS")) want_sets = (uint32_t)std::max(1, std::min((int)kMaxPassSets, atoi(e)));
 #endif
-    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets);
+    size_t held = 16ull * c->out_cap;
+    for (const zrt_context::PassSet& ps : c->set)
+        held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk_cap + ps.hit_cap) + 4ull * ps.wfc_cap;
+    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets, held);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     const uint64_t T = s_pass * P;
     int rc;
@@ -1781,7 +1795,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // path, and the fallback).
     const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK);
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
-#ifdef ZRT_SWEEP
+#if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
