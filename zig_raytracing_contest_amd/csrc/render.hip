@@ -52,6 +52,10 @@ constexpr int kTraceBlock = 512;                     // launch bound of wf_kerne
 constexpr int kTraceThreads = 256;                   // threads per wf_kernel / trace_kernel block
 constexpr int kTriBatch = 2;                         // triangle loads in flight per lane
 constexpr int kParkBlock = 1024;                     // wf_park_kernel: one workgroup per CU
+#ifndef ZRT_SHADE_N
+#define ZRT_SHADE_N 2
+#endif
+constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue entries per lane per fetch
 
 struct TraceParams {
     float bmin[3], bmax[3];
@@ -964,6 +968,34 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 // after traceRay, stage3.zig:195-219) over the hit records wf_park_kernel
 // wrote, one lane per path with every lane of the wave busy, appending the
 // continuing paths to the next queue.  Same XCD group order as the trace.
+// One queue entry of the shading half: its path record (a, b, c) and hit
+// record h already loaded; shades, writes the terminal radiance of an ending
+// path and appends a continuing one (the whole wave calls it).
+__device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf, bool valid,
+                                            float4 a, float4 b, float4 c, float4 h, uint64_t below,
+                                            uint32_t grp, uint32_t& n_seg) {
+    bool cont = false;
+    uint32_t item = 0, depth = 0, slot = 0, mask = 0;
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+    Rng rng;
+    rng.s = 0;
+    if (valid) {
+        o = mk(a.x, a.y, a.z);
+        item = __float_as_uint(a.w);
+        d = mk(b.x, b.y, b.z);
+        depth = __float_as_uint(b.w) & 0xFFFFu;
+        slot = __float_as_uint(b.w) >> 16;
+        rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+        mask = __float_as_uint(c.z);
+        v3 L = mk(0, 0, 0);
+        ++n_seg;                               // queued paths have depth >= 1
+        cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot, rng,
+                             mask, L);
+        if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
+    }
+    wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
+}
+
 __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -977,35 +1009,27 @@ __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w)
     uint32_t grp = blockIdx.x & 7u, tried = 0;
     WfParams ws = w;
     ws.fetch8 = w.fetch8s;
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // kShadeEntries entries per lane per fetch: every entry's records are
+    // loaded before the first is shaded, so their latency overlaps the
+    // earlier entries' dependent chains (2: cfg3 +1.2%, cfg2 / cfg5 within
+    // noise, 112 VGPRs, r02c6)
     for (;;) {
         uint32_t base = 0, lim = 0;
-        if (!wf_fetch<false>(ws, 64u, grp, tried, base, lim)) break;
-        const uint32_t j = base + lane;
-        bool cont = false;
-        uint32_t item = 0, depth = 0, slot = 0, mask = 0;
-        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-        Rng rng;
-        rng.s = 0;
-        if (j < lim) {
-            const uint32_t i = ent_index<false>(p, grp, j);
-            const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1], c = w.q_in[3ull * i + 2];
-            o = mk(a.x, a.y, a.z);
-            item = __float_as_uint(a.w);
-            d = mk(b.x, b.y, b.z);
-            depth = __float_as_uint(b.w) & 0xFFFFu;
-            slot = __float_as_uint(b.w) >> 16;
-            rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-            mask = __float_as_uint(c.z);
-            v3 L = mk(0, 0, 0);
-            {                                  // queued paths have depth >= 1
-                ++n_seg;
-                const float4 h = w.hit[i];
-                cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot,
-                                     rng, mask, L);
+        if (!wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim)) break;
+        float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
+#pragma unroll
+        for (int e = 0; e < kShadeEntries; ++e) {
+            const uint32_t j = base + 64u * e + lane;
+            a[e] = b[e] = c[e] = h[e] = z4;
+            if (j < lim) {
+                const uint32_t i = ent_index<false>(p, grp, j);
+                a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2]; h[e] = w.hit[i];
             }
-            if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
         }
-        wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
+#pragma unroll
+        for (int e = 0; e < kShadeEntries; ++e)
+            shade_entry(w, zx, zf, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
