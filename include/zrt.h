@@ -104,8 +104,9 @@ typedef struct zrt_render_config {
     uint32_t num_ranks;              /* tiles t with t % num_ranks == rank */
     uint32_t tile_size;              /* square tile edge in pixels, 0 = 64 */
     uint32_t flags;                  /* ZRT_FLAG_* */
-    uint32_t samples_per_pass;       /* samples of every pixel per device pass, 0 = as many as fit
-                                        40 GiB of path queues (the image is the same for any value) */
+    uint32_t samples_per_pass;       /* samples of every pixel per device pass, 0 = automatic: as few
+                                        passes as 144 GiB of path queues allow, at least two for frames
+                                        of 2^23 samples or more (the image is the same for any value) */
     uint32_t _reserved[4];
 } zrt_render_config;
 
@@ -168,7 +169,11 @@ void zrt_geometry_free(zrt_geometry* g);
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_render_config* cfg,
                uint8_t* rgb_out, zrt_stats* stats);
 
-/* Device-resident path (scene uploaded once, many renders). */
+/* Device-resident path (scene uploaded once, many renders).  A context owns
+ * its HIP streams: frames of 2^23 samples or more run their passes on two
+ * streams (two pass sets, each with its own queues); zrt_context_render
+ * returns once every stream is done, and device_rgb_packed is written on the
+ * context's main stream after the join.  One thread at a time per context. */
 typedef struct zrt_context zrt_context;
 
 typedef struct zrt_outputs {

@@ -968,32 +968,33 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 // after traceRay, stage3.zig:195-219) over the hit records wf_park_kernel
 // wrote, one lane per path with every lane of the wave busy, appending the
 // continuing paths to the next queue.  Same XCD group order as the trace.
-// One queue entry of the shading half: its path record (a, b, c) and hit
-// record h already loaded; shades, writes the terminal radiance of an ending
-// path and appends a continuing one (the whole wave calls it).
-__device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf, bool valid,
-                                            float4 a, float4 b, float4 c, float4 h, uint64_t below,
-                                            uint32_t grp, uint32_t& n_seg) {
+// One path of the shading half, its state decoded and its hit record h
+// loaded: shades, writes the terminal radiance of an ending path and appends
+// a continuing one (the whole wave calls it).
+__device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, const double* zf, bool valid,
+                                           uint32_t item, v3 o, v3 d, uint32_t depth, uint32_t slot, Rng rng,
+                                           uint32_t mask, float4 h, uint64_t below, uint32_t grp,
+                                           uint32_t& n_seg) {
     bool cont = false;
-    uint32_t item = 0, depth = 0, slot = 0, mask = 0;
-    v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    Rng rng;
-    rng.s = 0;
     if (valid) {
-        o = mk(a.x, a.y, a.z);
-        item = __float_as_uint(a.w);
-        d = mk(b.x, b.y, b.z);
-        depth = __float_as_uint(b.w) & 0xFFFFu;
-        slot = __float_as_uint(b.w) >> 16;
-        rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-        mask = __float_as_uint(c.z);
         v3 L = mk(0, 0, 0);
-        ++n_seg;                               // queued paths have depth >= 1
+        ++n_seg;                               // queued / primary paths have depth >= 1
         cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot, rng,
                              mask, L);
         if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
     }
     wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
+}
+
+// One queue entry: its path record (a, b, c) and hit record h already loaded.
+__device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf, bool valid,
+                                            float4 a, float4 b, float4 c, float4 h, uint64_t below,
+                                            uint32_t grp, uint32_t& n_seg) {
+    Rng rng;
+    rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+    shade_path(w, zx, zf, valid, __float_as_uint(a.w), mk(a.x, a.y, a.z), mk(b.x, b.y, b.z),
+               __float_as_uint(b.w) & 0xFFFFu, __float_as_uint(b.w) >> 16, rng, __float_as_uint(c.z), h, below,
+               grp, n_seg);
 }
 
 __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
