@@ -673,7 +673,10 @@ __device__ __forceinline__ bool occx_cell(unsigned long long bm, const D& s) {
 // r02k ISA).  Nothing orders an LDS read behind a pending LDS-DMA but the
 // wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
 constexpr int kParkWaves = kParkBlock / 64;
-constexpr uint32_t kParkChunk = 64;    // queue entries per work atomic of a park wave
+#ifndef ZRT_PARK_CHUNK
+#define ZRT_PARK_CHUNK 64
+#endif
+constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;    // queue entries per work atomic of a park wave
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
 // a store whose VGPR operands are read late, so whenever the register
