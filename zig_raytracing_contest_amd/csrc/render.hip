@@ -56,6 +56,12 @@ constexpr int kParkBlock = 1024;                     // wf_park_kernel: one work
 #define ZRT_SHADE_N 2
 #endif
 constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue entries per lane per fetch
+#ifndef ZRT_WF_CHUNK
+#define ZRT_WF_CHUNK 2
+#endif
+// wf_kernel: 64-entry batches per work atomic (r02d1: 2 vs 1 cfg3 +0.35%,
+// cfg2 +0.9%, cfg5 +0.2%; 4: +0.6 / +0.5 / 0%)
+constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 
 struct TraceParams {
     float bmin[3], bmax[3];
@@ -551,8 +557,9 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 
     for (;;) {
         uint32_t base = 0, lim = 0;
-        if (!wf_fetch<PRIMARY>(w, 64u, grp, tried, base, lim)) break;
-        const uint32_t j = base + lane;
+        if (!wf_fetch<PRIMARY>(w, 64u * kWfChunk, grp, tried, base, lim)) break;
+      for (uint32_t sub = 0; sub < kWfChunk && base + 64u * sub < lim; ++sub) {
+        const uint32_t j = base + 64u * sub + lane;
         const bool valid = j < lim;
         const uint32_t i = valid ? ent_index<PRIMARY>(p, grp, j) : 0u;
         bool cont = false;
@@ -591,6 +598,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
         }
         wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask, grp);
+      }
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -674,9 +682,11 @@ __device__ __forceinline__ bool occx_cell(unsigned long long bm, const D& s) {
 // wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
 constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_CHUNK
-#define ZRT_PARK_CHUNK 64
+#define ZRT_PARK_CHUNK 128
 #endif
-constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;    // queue entries per work atomic of a park wave
+// queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
+// 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%)
+constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
 // a store whose VGPR operands are read late, so whenever the register
