@@ -1119,8 +1119,14 @@ using WfFn = void (*)(const WfParams);
 // (ZRT_FLAG_LANE_WALK) at 6: 7 waves put 2-3 spill reloads in that walk and
 // ran cfg3 at 1933 vs 2108 (round 1).  tests/test_codegen.py checks every
 // instantiation zrt_timed_kernels names.
-constexpr int kWfMinWaves = 6;
-constexpr int kWfMinWaves0 = 7;
+#ifndef ZRT_WF_MINW
+#define ZRT_WF_MINW 6
+#endif
+#ifndef ZRT_WF_MINW0
+#define ZRT_WF_MINW0 7
+#endif
+constexpr int kWfMinWaves = ZRT_WF_MINW;
+constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
 // wf_park_kernel schedule: a test round once 12 lanes are parked, a shade +
 // refill round once 16 lanes are finished (cfg3 64 spp sweep, r02d: T 4-16 x
 // R 8/16/32; T 12 R 16 3110 Mrays/s, T 8-16 R 16 within 1.3%, R 8 -15%,
@@ -1276,8 +1282,8 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    static_assert(kWfMinWaves0 == 7 && kWfMinWaves == 6, "update the strings below");
-    return "wf_kernelILi" ZRT_STR(7) "ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(6) "ELb0EE";
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(
+        ZRT_WF_MINW) "ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
