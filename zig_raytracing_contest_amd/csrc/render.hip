@@ -1175,6 +1175,13 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kPassSets = 2;
 constexpr uint32_t kMaxPassSets = 4;
 constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that runs kPassSets
+// % of a pass moved from the last pass to the first when two sets run (r02d7,
+// vs 0: 20% cfg3 +3.2%, cfg5 +0.2%, cfg2 -1.0%; 16% cfg3 +1.4%; 25% cfg3
+// +3.2%, cfg2 -1.7%; the response is bumpy: r02d5/d6 sweeps)
+#ifndef ZRT_LEAD_PCT
+#define ZRT_LEAD_PCT 20
+#endif
+constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 128 * 4 - 256;
 
@@ -1789,14 +1796,31 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk_cap + ps.hit_cap) + 4ull * ps.wfc_cap;
     const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets, held);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
-    const uint64_t T = s_pass * P;
-    int rc;
     // pass sets: pass p runs on set p % nsets, each set with its own stream
     // and buffers, so one pass's launches fill the machine while another's
     // drain (tails, the latency-bound shade kernel beside the park kernel):
     // two sets cfg3 -5%, cfg2 -9%, cfg5 -7% frame time, images identical
     // (r02c1, profiles/r02/r02c1_ab_two_streams.log)
     const uint32_t nsets = counting ? 1u : std::min<uint32_t>(npasses, want_sets);
+    // lead: samples moved from the last pass to the first.  The second set's
+    // first primary launch waits for the first's (it fills every CU), so the
+    // second set ends behind the first unless the first has more work.
+    uint32_t lead_pct = nsets > 1 ? kLeadPct : 0u;
+#if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
+    if (const char* e = getenv("ZRT_LEAD")) lead_pct = nsets > 1 ? (uint32_t)std::max(0, std::min(50, atoi(e))) : 0u;
+#endif
+    const uint64_t last_n = spp - (uint64_t)(npasses - 1) * s_pass;     // samples of the last pass
+    const uint64_t cap_items = std::max<uint64_t>(1, 0x7FFFFF00ull / P);
+    const uint32_t lead = npasses > 1 ? (uint32_t)std::min<uint64_t>(
+                                            {s_pass * lead_pct / 100, last_n - 1, cap_items - std::min(cap_items, s_pass)})
+                                      : 0u;
+    auto pass_first = [&](uint32_t pass) -> uint32_t { return pass == 0 ? 0u : (uint32_t)(pass * s_pass + lead); };
+    auto pass_count = [&](uint32_t pass) -> uint32_t {
+        return pass == 0 ? (uint32_t)std::min<uint64_t>(spp, s_pass + lead)
+                         : (uint32_t)std::min<uint64_t>(s_pass, spp - pass_first(pass));
+    };
+    const uint64_t T = (s_pass + lead) * P;      // the first pass is the largest
+    int rc;
     if (counting && (rc = grow(&c->d_out, &c->out_cap, (size_t)T)) != ZRT_OK) return rc;
     for (uint32_t k = 0; k < nsets && !counting; ++k) {
         zrt_context::PassSet& ps = c->set[k];
@@ -1931,8 +1955,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         float4* const stk = ps.stk;
         uint32_t* const wfc = ps.wfc;
         float4* const hit = ps.hit;
-        const uint32_t s0 = (uint32_t)(pass * s_pass);
-        const uint32_t S = (uint32_t)std::min<uint64_t>(s_pass, spp - s0);
+        const uint32_t s0 = pass_first(pass);
+        const uint32_t S = pass_count(pass);
         tp.s0 = s0;
         tp.total = S * P;
         const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
