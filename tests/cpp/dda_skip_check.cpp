@@ -56,19 +56,28 @@ static uint64_t g_walk_fails = 0, g_walk_steps = 0;
 
 // DDAW_STEP (the park kernel's walk) against DDA_STEP, step by step: cells,
 // linear index, crossing flag, T_EXIT and the next crossing ts bit for bit
+// and DDAP_STEP (the packed cell of the park walk) the same way: packed cell,
+// linear index, crossing flag, T_EXIT and ts bit for bit up to the exit step
+// (past it the packed fields may carry; the walk has ended there)
 static void walk_w(const GridK& k, Dda s) {
     DdaW w;
     ddaw_from(s, k, w);
+    DdaP q;
+    ddap_from(s, k, q);
     for (int guard = 0; guard < 100000; ++guard) {
-        bool c1, c2;
-        float e1, e2;
+        bool c1, c2, c3;
+        float e1, e2, e3;
         DDA_STEP(s, k, 2, c1, e1);
         DDAW_STEP(w, 2, c2, e2);
+        DDAP_STEP(q, kPackLow2, c3, e3);
         ++g_walk_steps;
         const bool same = c1 == c2 && !memcmp(&e1, &e2, 4) && s.c0 == w.c0 && s.c1 == w.c1 && s.c2 == w.c2 &&
                           s.lin == w.lin && !memcmp(&s.tn0, &w.tn0, 4) && !memcmp(&s.tn1, &w.tn1, 4) &&
                           !memcmp(&s.tn2, &w.tn2, 4);
-        if (!same) {
+        const bool same_p = !memcmp(&e1, &e3, 4) && s.lin == q.lin && !memcmp(&s.tn0, &q.tn0, 4) &&
+                            !memcmp(&s.tn1, &q.tn1, 4) && !memcmp(&s.tn2, &q.tn2, 4) &&
+                            (e1 == kInf || (c1 == c3 && q.pc == pack_cell(s.c0, s.c1, s.c2)));
+        if (!same || !same_p) {
             ++g_walk_fails;
             return;
         }

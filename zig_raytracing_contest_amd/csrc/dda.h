@@ -165,6 +165,71 @@ ZHD void ddaw_from(const Dda& d, const GridK& g, DdaW& w) {
         (D).l1 = (C) ? (A).l1 : (B).l1; (D).l2 = (C) ? (A).l2 : (B).l2;              \
     } while (0)
 
+// The park walk's state with the cell packed into one word (grids of at most
+// 1024 cells per axis): pc = c0 | c1 << 10 | c2 << 20.  A step adds the
+// axis's packed step d_a (+-1 << 10a mod 2^32), the crossing test is one xor
+// and mask, the exit test compares the axis's field with the packed exit
+// cells pe.  Same booleans, same f32 adds, same cells, linear index and
+// T_EXIT as DDAW_STEP (tests/cpp/dda_skip_check.cpp).  A step past the exit
+// (T_EXIT = +inf) may carry into the next field; the walk ends there, and
+// the park kernel's speculative second step only reads a clamped brick.
+struct DdaP {
+    float tn0, tn1, tn2, td0, td1, td2;
+    uint32_t pc, lin, pe;
+    uint32_t d0, d1, d2;      // packed cell step per axis
+    uint32_t s0, l1, l2;      // linear-index step per axis (axis 0: s0)
+};
+constexpr uint32_t kPackF0 = 0x3FFu, kPackF1 = 0x3FFu << 10, kPackF2 = 0x3FFu << 20;
+constexpr uint32_t kPackLow2 = 3u | (3u << 10) | (3u << 20);   // in-brick bits, 4^3 bricks
+constexpr uint32_t kPackMaxRes = 1024;                         // cells per axis a DdaP holds
+ZHD uint32_t pack_cell(uint32_t c0, uint32_t c1, uint32_t c2) { return c0 | (c1 << 10) | (c2 << 20); }
+ZHD void ddap_from(const Dda& d, const GridK& g, DdaP& w) {
+    w.tn0 = d.tn0; w.tn1 = d.tn1; w.tn2 = d.tn2;
+    w.td0 = d.td0; w.td1 = d.td1; w.td2 = d.td2;
+    w.pc = pack_cell(d.c0, d.c1, d.c2);
+    w.lin = d.lin;
+    const bool n0 = d.neg & 1u, n1 = (d.neg >> 1) & 1u, n2 = (d.neg >> 2) & 1u;
+    w.pe = pack_cell(n0 ? 0u : g.rm0, n1 ? 0u : g.rm1, n2 ? 0u : g.rm2);
+    w.d0 = n0 ? 0xFFFFFFFFu : 1u;
+    w.d1 = n1 ? 0u - (1u << 10) : (1u << 10);
+    w.d2 = n2 ? 0u - (1u << 20) : (1u << 20);
+    w.s0 = w.d0;
+    w.l1 = n1 ? 0u - g.str1 : g.str1;
+    w.l2 = n2 ? 0u - g.str2 : g.str2;
+}
+// LOWM: the in-brick bits of every field (4^3 bricks: 3 | 3 << 10 | 3 << 20)
+#define DDAP_STEP(S, LOWM, CROSSED, T_EXIT)                                            \
+    do {                                                                             \
+        const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
+        const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
+        const bool a0_ = b01_ && b02_;                                               \
+        const bool a1_ = !b01_ && b12_;                                              \
+        const bool a2_ = !a0_ && !a1_;                                               \
+        const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
+        const float dt_ = a0_ ? (S).td0 : (a1_ ? (S).td1 : (S).td2);                 \
+        const uint32_t fm_ = a0_ ? kPackF0 : (a1_ ? kPackF1 : kPackF2);              \
+        const uint32_t pn_ = (S).pc + (a0_ ? (S).d0 : (a1_ ? (S).d1 : (S).d2));      \
+        (S).lin += a0_ ? (S).s0 : (a1_ ? (S).l1 : (S).l2);                           \
+        (CROSSED) = (((S).pc ^ pn_) & ~(LOWM)) != 0u;                                \
+        (T_EXIT) = (((S).pc ^ (S).pe) & fm_) == 0u ? kInf : tc_;                     \
+        const float un_ = tc_ + dt_;                                                 \
+        (S).tn0 = a0_ ? un_ : t0_;                                                   \
+        (S).tn1 = a1_ ? un_ : t1_;                                                   \
+        (S).tn2 = a2_ ? un_ : t2_;                                                   \
+        (S).pc = pn_;                                                                \
+    } while (0)
+#define DDAP_SEL(D, C, A, B)                                                          \
+    do {                                                                             \
+        (D).tn0 = (C) ? (A).tn0 : (B).tn0; (D).tn1 = (C) ? (A).tn1 : (B).tn1;        \
+        (D).tn2 = (C) ? (A).tn2 : (B).tn2; (D).td0 = (C) ? (A).td0 : (B).td0;        \
+        (D).td1 = (C) ? (A).td1 : (B).td1; (D).td2 = (C) ? (A).td2 : (B).td2;        \
+        (D).pc = (C) ? (A).pc : (B).pc; (D).lin = (C) ? (A).lin : (B).lin;           \
+        (D).pe = (C) ? (A).pe : (B).pe; (D).d0 = (C) ? (A).d0 : (B).d0;              \
+        (D).d1 = (C) ? (A).d1 : (B).d1; (D).d2 = (C) ? (A).d2 : (B).d2;              \
+        (D).s0 = (C) ? (A).s0 : (B).s0; (D).l1 = (C) ? (A).l1 : (B).l1;              \
+        (D).l2 = (C) ? (A).l2 : (B).l2;                                              \
+    } while (0)
+
 // Empty-brick skip, 4^3 bricks (occ_shift 2): the state Iterator.next would
 // reach at the step that leaves the current brick, computed at once.  Axis
 // a's crossings form the sequence T_a(1) = tn_a, T_a(j+1) = T_a(j) + td_a

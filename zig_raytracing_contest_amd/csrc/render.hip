@@ -664,6 +664,16 @@ template <class D>
 __device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const D& s) {
     return __umul24(s.c2 >> 2, w.occx_nb01) + __umul24(s.c1 >> 2, w.occx_nb0) + (s.c0 >> 2);
 }
+// the same two from a packed cell (DdaP, fields of 10 bits)
+__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaP& s) {
+    return __umul24((s.pc >> 22) & 0xFFu, w.occx_nb01) + __umul24((s.pc >> 12) & 0xFFu, w.occx_nb0) +
+           ((s.pc >> 2) & 0xFFu);
+}
+__device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaP& s) {
+    const uint32_t half = (s.pc & (2u << 20)) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
+    const uint32_t k = ((s.pc >> 16) & 0x10u) | ((s.pc >> 8) & 0xCu) | (s.pc & 3u);
+    return (half >> k) & 1u;
+}
 // bit of cell (c0, c1, c2) in its brick's 64-bit mask, tested on the 32-bit
 // half that holds it (bit 5 of the index is bit 1 of c2)
 template <class D>
@@ -788,7 +798,17 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t cb = 0, ce = 0, cgrp = 0;     // the wave's current chunk of queue entries
     // the segment: ray, DDA state, current brick's cell mask, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+#ifdef ZRT_UNPACKED_WALK
     DdaW s;
+#define PARK_FROM ddaw_from
+#define PARK_STEP(S, CR, TE) DDAW_STEP(S, 2u, CR, TE)
+#define PARK_SEL DDAW_SEL
+#else
+    DdaP s;                                // grids of <= 1024 cells per axis (zrt_context_render)
+#define PARK_FROM ddap_from
+#define PARK_STEP(S, CR, TE) DDAP_STEP(S, kPackLow2, CR, TE)
+#define PARK_SEL DDAP_SEL
+#endif
     memset(&s, 0, sizeof s);
     unsigned long long bm = 0ull;
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
@@ -845,7 +865,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
                             Dda s0;
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
-                                ddaw_from(s0, gk, s);
+                                PARK_FROM(s0, gk, s);
                                 bm = occx_mask(L, occx_brick(w, s));
                                 if (occx_cell(bm, s)) {
                                     park_load_range(p, s.lin, rng_slot);
@@ -881,12 +901,12 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // chain of LDS latencies for two cells; the second step is
                 // speculative and dropped when the first cell parks or ends
                 // the segment (its lookup then reads a clamped brick)
-                DdaW s1 = s;
+                auto s1 = s;
                 bool cr1, cr2;
                 float te1, te2;
-                DDAW_STEP(s1, 2u, cr1, te1);
-                DdaW s2 = s1;
-                DDAW_STEP(s2, 2u, cr2, te2);
+                PARK_STEP(s1, cr1, te1);
+                auto s2 = s1;
+                PARK_STEP(s2, cr2, te2);
                 unsigned long long q1 = occx_mask_clamped(L, occx_brick(w, s1), w.occx_nbw);
                 unsigned long long q2 = occx_mask_clamped(L, occx_brick(w, s2), w.occx_nbw);
                 // both lookups complete here, ahead of the selects below
@@ -904,7 +924,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const bool at1 = d1 || o1;
                 const bool pk = at1 ? !d1 : (!d2 && o2);
                 if (at1 ? d1 : d2) st = kDone;
-                DDAW_SEL(s, at1, s1, s2);
+                PARK_SEL(s, at1, s1, s2);
                 bm = at1 ? m1 : m2;
                 if (pk) {                                          // one issue point per trip
                     park_load_range(p, s.lin, rng_slot);
@@ -971,6 +991,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         PARK_STAMP(2);
     }
     __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
+#undef PARK_FROM
+#undef PARK_STEP
+#undef PARK_SEL
 #ifdef ZRT_SWEEP
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
@@ -1861,7 +1884,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // (coherent 8x8-pixel waves: 22 vs 42 ms for the park kernel at cfg3 64
     // spp, r02d).  ZRT_FLAG_LANE_WALK: wf_kernel for every launch (round 1's
     // path, and the fallback).
-    const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK);
+    // (the park walk packs a cell into one word: at most 1024 cells per axis)
+    const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK) &&
+                           c->grid.resolution[0] <= kPackMaxRes && c->grid.resolution[1] <= kPackMaxRes &&
+                           c->grid.resolution[2] <= kPackMaxRes;
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
