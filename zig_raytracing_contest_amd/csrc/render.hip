@@ -120,6 +120,15 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
+// brick_occupied for a packed cell (DdaP, 10 bits per axis)
+__device__ __forceinline__ bool brick_occupied_p(const TraceParams& p, const uint32_t* occ, uint32_t pc) {
+    const uint32_t s = p.occ_shift;
+    const uint32_t m = 0x3FFu >> s;
+    const uint32_t b = __umul24((pc >> (20u + s)) & m, p.occ_nb01) + __umul24((pc >> (10u + s)) & m, p.occ_nb0) +
+                       ((pc >> s) & m);
+    return (occ[b >> 5] >> (b & 31u)) & 1u;
+}
+
 // Grid constants as wave-uniform registers (see GridK).
 __device__ __forceinline__ GridK grid_consts(const TraceParams& p) {
     GridK g;
@@ -174,7 +183,9 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // [6] cell loads, [7] non-empty cells, [8] wave trips of the cell loop,
 // [9] wave trips of the triangle-batch loop, [10] cell trips with any test,
 // [4] 64-wide rounds if each trip's tests were shared evenly.
-template <bool STATS, int TB>
+// PACKED: the walk state with the cell packed into one word (DdaP, grids of
+// at most 1024 cells per axis; same cells, same order, same t_exit).
+template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr) {
@@ -183,6 +194,25 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
     if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
     const uint32_t sh = p.occ_shift;
     const GridK gk = grid_consts(p);
+    if constexpr (PACKED) {
+        static_assert(!STATS, "the counting build walks unpacked");
+        DdaP s;
+        ddap_from(s0, gk, s);
+        const uint32_t lowm = ((1u << sh) - 1u) * (1u | (1u << 10) | (1u << 20));
+        bool occupied = brick_occupied_p(p, occ, s.pc);
+        for (;;) {
+            if (occupied) {
+                const uint2 cell = p.cells[s.lin];
+                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+            }
+            bool crossed;
+            float t_exit;
+            DDAP_STEP(s, lowm, crossed, t_exit);
+            if (nearest <= t_exit) break;                  // stage3.zig:179-182
+            if (crossed) occupied = brick_occupied_p(p, occ, s.pc);
+        }
+        return nearest;
+    }
     DdaW s;
     ddaw_from(s0, gk, s);
     bool occupied = brick_occupied(p, occ, s.c0, s.c1, s.c2);
@@ -540,7 +570,7 @@ __device__ __forceinline__ void path_state(const WfParams& w, uint32_t i, uint32
 }
 
 // wf_kernel: one lane = one segment, walked and tested by the lane itself.
-template <int MINW, bool PRIMARY>
+template <int MINW, bool PRIMARY, bool PACKED>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -585,7 +615,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             float t = kInf, hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
             if (depth != 0)
-                t = trace_ray<false, kTriBatch>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
+                t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
             uint32_t item, slot;
             Rng rng;
             path_state<PRIMARY>(w, i, item, depth, slot, rng, mask);
@@ -1157,8 +1187,11 @@ constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
 // ZRT_PARK_T / ZRT_PARK_R.
 constexpr uint32_t kParkTestMin = 12;
 constexpr uint32_t kParkRefillMin = 16;
-const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true>;
-const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false>;
+// packed walk state when every axis has at most kPackMaxRes cells
+const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true, true>;
+const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false, true>;
+const WfFn kWfPrimaryWide = (WfFn)wf_kernel<kWfMinWaves0, true, false>;
+const WfFn kWfBounceWide = (WfFn)wf_kernel<kWfMinWaves, false, false>;
 
 // max_bounce picks the stack depth the counting kernel is compiled for.
 TraceFn count_fn(uint32_t max_bounce) {
@@ -1312,8 +1345,8 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(
-        ZRT_WF_MINW) "ELb0EE";
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(
+        ZRT_WF_MINW) "ELb0ELb1EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
@@ -1893,8 +1926,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
-    const WfFn f_first = kWfPrimary;
-    const WfFn f_next = park_next ? (WfFn)wf_park_kernel : kWfBounce;
+    const bool packed = c->grid.resolution[0] <= kPackMaxRes && c->grid.resolution[1] <= kPackMaxRes &&
+                        c->grid.resolution[2] <= kPackMaxRes;
+    const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
+    const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
     const WfFn s_next = (WfFn)wf_shade_kernel;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
         if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
