@@ -197,6 +197,16 @@ ZHD void ddap_from(const Dda& d, const GridK& g, DdaP& w) {
     w.l1 = n1 ? 0u - g.str1 : g.str1;
     w.l2 = n2 ? 0u - g.str2 : g.str2;
 }
+// An opaque copy: keeps the compiler from merging `a0 ? t2 : (a1 ? t2 : u)`
+// into `(a0 || a1) ? t2 : u`, whose or-of-compares it turns into a select of
+// booleans materialised in VGPRs (7 VALU per step in the r02e5 ISA instead of
+// the second v_cndmask).
+ZHD float opaque_f(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(x));
+#endif
+    return x;
+}
 // LOWM: the in-brick bits of every field (4^3 bricks: 3 | 3 << 10 | 3 << 20)
 #define DDAP_STEP(S, LOWM, CROSSED, T_EXIT)                                            \
     do {                                                                             \
@@ -215,7 +225,8 @@ ZHD void ddap_from(const Dda& d, const GridK& g, DdaP& w) {
         const float un_ = tc_ + dt_;                                                 \
         (S).tn0 = a0_ ? un_ : t0_;                                                   \
         (S).tn1 = a1_ ? un_ : t1_;                                                   \
-        (S).tn2 = a2_ ? un_ : t2_;                                                   \
+        (S).tn2 = a0_ ? t2_ : (a1_ ? opaque_f(t2_) : un_);    /* a2_: neither */     \
+        (void)a2_;                                                                   \
         (S).pc = pn_;                                                                \
     } while (0)
 #define DDAP_SEL(D, C, A, B)                                                          \
