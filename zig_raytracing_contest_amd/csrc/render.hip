@@ -672,20 +672,19 @@ struct OccX {
     const uint2* ent;                    // (brick bits, occupied bricks before the word)
     const unsigned long long* masks;
 };
-__device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
-    const uint2 e = L.ent[b >> 5];
-    const uint32_t r = e.y + (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
-    const unsigned long long m = L.masks[r];            // r <= occupied count: the zero mask at worst
+__device__ __forceinline__ unsigned long long occx_mask_at(const OccX& L, uint2 e, uint32_t b) {
+    const uint32_t below = (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
+    const unsigned long long m = L.masks[e.y + below];  // <= occupied count: the zero mask at worst
     return ((e.x >> (b & 31u)) & 1u) ? m : 0ull;
+}
+__device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
+    return occx_mask_at(L, L.ent[b >> 5], b);
 }
 // occx_mask for a brick index that may lie past the grid (a speculative
 // step beyond the exit cell): the word index is clamped into the blob, so
 // the read stays inside it; the result of such a lookup is never used
 __device__ __forceinline__ unsigned long long occx_mask_clamped(const OccX& L, uint32_t b, uint32_t nbw) {
-    const uint2 e = L.ent[min(b >> 5, nbw - 1u)];
-    const uint32_t r = e.y + (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
-    const unsigned long long m = L.masks[r];
-    return ((e.x >> (b & 31u)) & 1u) ? m : 0ull;
+    return occx_mask_at(L, L.ent[min(b >> 5, nbw - 1u)], b);
 }
 // brick index: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate),
 // exact because a grid of more than 2^24 bricks is rejected at context
