@@ -115,8 +115,8 @@ def _loops(ins):
 
 def test_park_walk_trip_is_not_a_register_shuffle(code):
     """The walk trip (two DDA steps, two OccX lookups = 4 LDS reads, one range
-    DMA issue point) stays ~123 VALU (143 before the packed cell, 130 before
-    the opaque third-axis select).  Its old branchy form let the compiler
+    DMA issue point) stays ~115 VALU (143 before the packed cell, 130 before
+    the opaque third-axis select, 123 with a brick-mask select).  Its old branchy form let the compiler
     copy the whole walk state through every join: a one-line change elsewhere
     in the kernel took it from 160 to 232 VALU (96 v_mov) and cfg3 lost 2-3%
     with identical images."""

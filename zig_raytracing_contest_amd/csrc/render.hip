@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     bool more = true;
     uint32_t grp = blockIdx.x & 7u, tried = 0;
     uint32_t cb = 0, ce = 0, cgrp = 0;     // the wave's current chunk of queue entries
-    // the segment: ray, DDA state, current brick's cell mask, best hit, range
+    // the segment: ray, DDA state, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
 #ifdef ZRT_UNPACKED_WALK
     DdaW s;
@@ -839,7 +839,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 #define PARK_SEL DDAP_SEL
 #endif
     memset(&s, 0, sizeof s);
-    unsigned long long bm = 0ull;
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
@@ -895,8 +894,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             Dda s0;
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
                                 PARK_FROM(s0, gk, s);
-                                bm = occx_mask(L, occx_brick(w, s));
-                                if (occx_cell(bm, s)) {
+                                if (occx_cell(occx_mask(L, occx_brick(w, s)), s)) {
                                     park_load_range(p, s.lin, rng_slot);
                                     st = kPark;
                                 } else {
@@ -942,8 +940,17 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // (left alone, the compiler sinks the second into the branch
                 // that uses it and the two LDS chains run one after the other)
                 asm volatile("" : "+v"(q1), "+v"(q2));
-                const unsigned long long m1 = cr1 ? q1 : bm;
-                const unsigned long long m2 = cr2 ? q2 : m1;
+                // a cell's lookup is its brick's mask whether or not the step
+                // crossed into a new brick (uncrossed: the same brick, the
+                // same mask), so the walk keeps no current-brick mask and
+                // selects nothing on the crossing (r02f3: 115 instead of 123
+                // VALU per trip); a step past the grid exit reads a clamped
+                // brick, but that step ends the segment (T_EXIT = +inf) and
+                // its mask is never tested
+                (void)cr1;
+                (void)cr2;
+                const unsigned long long m1 = q1;
+                const unsigned long long m2 = q2;
                 // the trip ends in the first of its cells that ends the
                 // segment (stage3.zig:179-182) or holds triangles; selects,
                 // not branches: the branchy form made the compiler copy the
@@ -954,7 +961,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const bool pk = at1 ? !d1 : (!d2 && o2);
                 if (at1 ? d1 : d2) st = kDone;
                 PARK_SEL(s, at1, s1, s2);
-                bm = at1 ? m1 : m2;
                 if (pk) {                                          // one issue point per trip
                     park_load_range(p, s.lin, rng_slot);
                     st = kPark;
