@@ -24,13 +24,17 @@ Beside the timed loop (rank 0, N = 1, after it):
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-wall-clock]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Rank 0 prints ONE JSON line.  Image tiles (64x64, interleaved t % N) shard the
-frame: total work is fixed as N grows ("scaling": "strong").
+Rank 0 prints ONE JSON line, with the sha1 of the whole frame (img_sha1: the
+same for any N, asserted equal to the untimed counting frame's).  Image tiles
+(64x64, interleaved t % N) shard the frame: total work is fixed as N grows
+("scaling": "strong").  The roofline block is the dominant kernel's, from one
+extra frame on one HIP stream (exclusive kernel durations).
 """
 from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import json
 import os
 import re
@@ -62,45 +66,13 @@ def parse():
     ap.add_argument("--spp", type=int, default=None, help="override spp (NOT the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wall-clock", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=24.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--one-set", action="store_true",
+                    help="time frames on one pass set (exclusive kernel durations: the rocprofv3 "
+                         "profile of the roofline, NOT the headline schedule)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1 process group; gloo (tests only) gathers host copies, ranks may share a GPU")
     return ap.parse_args()
-
-
-def traffic_for(config, kernel):
-    """Memory-side bytes per launch of `kernel` from the newest committed PMC
-    summary for this workload (tools/pmc_traffic.py over rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 corrections there)."""
-    best = None
-    # newest round tag last: r01 < r01i < r02e < r02m < r02aj (length, then name)
-    def tag_key(f):
-        t = os.path.basename(f).split("_traffic_")[0]
-        return (len(t), t)
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")), key=tag_key):
-        try:
-            with open(f) as fh:
-                t = json.load(fh)
-        except (OSError, ValueError):
-            continue
-        if kernel in t.get("kernel", ""):
-            best = (t["bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best
-
-
-def valu_for(config):
-    """VALU issue fraction per launch type (SURVEY.md d3's secondary figure)
-    from the newest committed SQ counter summary for this workload
-    (tools/gpu_r2round.sh: SQ_INSTS_VALU x 2 cycles / SIMD cycles)."""
-    files = glob.glob(os.path.join(ROOT, "profiles", "r02", f"r*_sq_counters_{config}_*.json"))
-    if not files:
-        return None
-    f = max(files, key=lambda x: (len(os.path.basename(x).split("_")[0]), os.path.basename(x)))
-    try:
-        with open(f) as fh:
-            d = json.load(fh)
-        return {"per_kernel": {k.rstrip("( "): v.get("_valu_issue_frac") for k, v in d["kernels"].items()},
-                "source": os.path.relpath(f, ROOT)}
-    except (OSError, ValueError, KeyError):
-        return None
 
 
 def cpu_model():
@@ -115,47 +87,70 @@ def cpu_model():
 
 
 def cpu_threads():
-    """All CPUs this process may use (the reference's num_threads null =
-    getCpuCount, main.zig:90), capped by OMP_NUM_THREADS when set: on the
-    shared GPU host that is the CPU share of one GPU."""
+    """The reference's thread count: config.json num_threads null means
+    getCpuCount (main.zig:90), and stage3.zig:248-252 spawns that many -- every
+    CPU in this process's affinity mask.  Also returns the OMP_NUM_THREADS cap
+    (on the shared GPU host, the CPU share of one GPU) for the secondary
+    figure."""
     avail = len(os.sched_getaffinity(0))
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return (min(avail, omp) if omp > 0 else avail), avail
+    return avail, (min(avail, omp) if omp > 0 else avail)
+
+
+def cgroup_cpu_quota():
+    """cgroup v2 cpu.max as CPUs (None: unlimited or unreadable): what the
+    all-core run can really use on a shared host."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(soup, cfg, target_s):
     """Oracle in REF mode (the reference's Xoshiro-per-thread, contiguous
     blocks, recursion; gcc -O3, no fast-math) on a bounded, evenly spread
-    sample of the same frame."""
+    sample of the same frame, on getCpuCount threads (all CPUs of the
+    affinity mask); the OMP_NUM_THREADS-capped run beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc   # test infrastructure: the CPU baseline leg only
     c = soup.camera(cfg["camera"])
     cam = orc.camera_from_matrix(c.matrix, c.yfov, c.aspect, cfg["width"], cfg["height"])
     osc = orc.OracleScene(soup)
-    threads, avail = cpu_threads()
+    threads, capped = cpu_threads()
     npx = cam.w * cam.h
 
-    def run(stride, spp):
+    def run(stride, spp, nthr):
         pixels = np.arange(0, npx, stride, dtype=np.uint32)
         t0 = time.perf_counter()
-        _, _, ctr = osc.render_pixels(cam, spp, cfg["max_bounce"], pixels, orc.RNG_REF, 0, threads)
+        _, _, ctr = osc.render_pixels(cam, spp, cfg["max_bounce"], pixels, orc.RNG_REF, 0, nthr)
         return time.perf_counter() - t0, ctr, pixels.size
 
-    dt, ctr, n = run(1024, 4)                   # calibration: ~2000 pixels x 4 spp
-    seg_rate = max(float(ctr[0]), 1.0) / max(dt, 1e-3)
-    seg_per_sample = max(float(ctr[0]) / (n * 4), 1.0)
-    want_samples = seg_rate * target_s / seg_per_sample
-    spp = 4
-    stride = max(1, int(npx * spp / max(want_samples, 1.0)))
-    if stride == 1:                             # whole frame: raise spp instead
-        spp = int(min(256, max(4, want_samples / npx)))
-    dt, ctr, n = run(stride, spp)
-    return {"value": round(float(ctr[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
-            "cores_available": avail, "nproc": os.cpu_count(), "cpu_model": cpu_model(), "kind": "port",
-            "sample": f"{n} pixels (every {stride}th of {cam.w}x{cam.h}) x {spp} spp, "
-                      f"{int(ctr[0])} segments in {dt:.1f}s; oracle REF mode (Xoshiro256++ per "
-                      f"thread, contiguous blocks, recursion), gcc -O3, {threads} threads "
-                      f"({avail} in the affinity mask; OMP_NUM_THREADS caps it on the GPU host)"}
+    def measure(nthr, secs):
+        dt, ctr, n = run(1024, 4, nthr)            # calibration: ~2000 pixels x 4 spp
+        seg_rate = max(float(ctr[0]), 1.0) / max(dt, 1e-3)
+        seg_per_sample = max(float(ctr[0]) / (n * 4), 1.0)
+        want_samples = seg_rate * secs / seg_per_sample
+        spp = 4
+        stride = max(1, int(npx * spp / max(want_samples, 1.0)))
+        if stride == 1:                             # whole frame: raise spp instead
+            spp = int(min(256, max(4, want_samples / npx)))
+        dt, ctr, n = run(stride, spp, nthr)
+        return float(ctr[0]) / dt / 1e6, (f"{n} pixels (every {stride}th of {cam.w}x{cam.h}) x {spp} spp, "
+                                          f"{int(ctr[0])} segments in {dt:.1f}s")
+
+    v, sample = measure(threads, target_s)
+    out = {"value": round(v, 3), "unit": "Mrays/s", "cores": threads, "cores_available": threads,
+           "cgroup_cpu_quota": cgroup_cpu_quota(), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "kind": "port",
+           "sample": f"{sample}; oracle REF mode (Xoshiro256++ per thread, contiguous blocks, "
+                     f"recursion), gcc -O3, {threads} threads = every CPU of the affinity mask "
+                     "(num_threads null -> getCpuCount, main.zig:90)"}
+    if capped < threads:
+        vc, sc = measure(capped, target_s / 2)
+        out["omp_capped"] = {"value": round(vc, 3), "cores": capped, "sample": sc,
+                             "what": "the same on OMP_NUM_THREADS threads (the GPU host's CPU share of one GPU)"}
+    return out
 
 
 _DUR = re.compile(r"(\d+(?:\.\d+)?)(ms|us|ns|s|m|h)")
@@ -242,19 +237,46 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def roofline_profile_for(config, one_set_kernel="wf_park_kernel"):
+    """The newest committed per-kernel counter profile of this workload
+    (tools/roofline_profile.py over rocprofv3 passes of `bench.py --one-set`:
+    exclusive kernel durations, SQ VALU counts, PMC HBM bytes per launch)."""
+    files = glob.glob(os.path.join(ROOT, "profiles", "r*", f"*_roofline_{config}.json"))
+    if not files:
+        return None
+    f = max(files, key=lambda x: (len(os.path.basename(x).split("_")[0]), os.path.basename(x)))
+    try:
+        with open(f) as fh:
+            d = json.load(fh)
+        return d, os.path.relpath(f, ROOT)
+    except (OSError, ValueError):
+        return None
+
+
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, a wave64 VALU instruction issues over
+# 2 cycles (32 lanes per cycle), 2.4 GHz peak engine clock: 78.6 T lane-ops/s
+# (the 157.3 TF f32 vector peak counts an FMA as 2 flops)
+PEAK_VALU_GLANE = 256 * 4 * 32 * 2.4
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = torch = None
+    gloo = a.backend == "gloo"
     if world > 1:
         # torch first: libzrt then binds to torch's HIP runtime (one runtime
         # per process, so the RCCL buffers and libzrt share device memory)
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:   # tests only: host copies gathered over gloo; ranks may share device 0
+            local = local % max(torch.cuda.device_count(), 1)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
     from zig_raytracing_contest_amd import dist as zdist
     cfgd = dict(scenes.CONFIGS[a.config])
@@ -264,32 +286,55 @@ def main():
     rs = RenderScene(soup, device=local)
     P = native.tile_pixels(cam.w, cam.h, 64, rank, world).size
     dev_buf = None
-    if world > 1:
+    if world > 1 and not gloo:
         dev_buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8,
                               device=f"cuda:{local}")
+    tflags = native.FLAG_ONE_SET if a.one_set else 0
 
-    def step(stats=False):
-        if world > 1:   # this rank's tiles into device memory + RCCL gather to rank 0
-            return zdist.render_gathered(rs.context, cam, spp, cfgd["max_bounce"], rank, world, dist,
-                                         dev_buf, stats=stats)[1]["stats"]
-        return rs.context.render(cam, spp, cfgd["max_bounce"], stats=stats)["stats"]
+    def step(stats=False, flags=tflags):
+        """One frame; returns (stats dict, image handle: the assembled frame on
+        rank 0 -- packed RGB8 at N = 1 -- or None)."""
+        if world > 1 and not gloo:   # this rank's tiles into device memory + RCCL gather to rank 0
+            img, res = zdist.render_gathered(rs.context, cam, spp, cfgd["max_bounce"], rank, world, dist,
+                                             dev_buf, stats=stats)
+            return res["stats"], img
+        res = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world, stats=stats,
+                                packed=True, flags=flags)
+        if world > 1:                # gloo: host copies
+            buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8)
+            buf[: res["packed"].size] = torch.from_numpy(res["packed"].reshape(-1))
+            return res["stats"], zdist.gather_image(buf, cam.w, cam.h, rank, world, dist)
+        return res["stats"], res["packed"]
+
+    def frame_sha1(img):
+        """sha1 of the whole w x h x 3 RGB8 frame (row-major): the same for any N."""
+        if img is None:
+            return None
+        if world == 1:
+            full = np.zeros((cam.w * cam.h, 3), np.uint8)
+            full[native.tile_pixels(cam.w, cam.h)] = img
+            return hashlib.sha1(full.tobytes()).hexdigest()
+        return hashlib.sha1(img.cpu().numpy().tobytes()).hexdigest()
 
     # untimed counting run: exact algorithmic work of one step (same RNG ->
-    # same paths as the timed kernels)
-    cst = step(stats=True)
+    # same paths as the timed kernels), and the frame every timed frame must equal
+    cst, cimg = step(stats=True)
+    cprof = rs.context.profile()
+    count_sha1 = frame_sha1(cimg) if rank == 0 else None
     for _ in range(a.warmup):
         step()
 
     def barrier():
         if world > 1:
             dist.barrier()
-            torch.cuda.synchronize()
+            if not gloo:
+                torch.cuda.synchronize()
 
     barrier()
     t0 = time.perf_counter()
-    kern_ms, gpu_ms, launches, segs = 0.0, 0.0, 0, 0
+    kern_ms, gpu_ms, launches, segs, img = 0.0, 0.0, 0, 0, None
     for _ in range(a.steps):
-        st = step()
+        st, img = step()
         kern_ms += st["trace_kernel_ms"]
         gpu_ms += st["render_ms"]
         launches += st["trace_launches"]
@@ -297,7 +342,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device=f"cuda:{local}")
+        dev = "cpu" if gloo else f"cuda:{local}"
+        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device=dev)
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -307,19 +353,80 @@ def main():
 
     if rank == 0:
         assert cst["segments"] * a.steps == segs, "counting and timed kernels disagree"
-        # two passes are in flight at once on two HIP streams (DESIGN.md
-        # §5), so launches overlap: a launch's share of the machine is the
-        # step's GPU time (HIP events from the first launch to the join of
-        # both streams) over its launches, and achieved = the step's
-        # algorithmic bytes over that GPU time.  The per-launch event
-        # intervals (what rocprofv3 reports as kernel durations, overlapped)
-        # are kept beside it.
-        avg_launch_s = gpu_ms / 1e3 / max(launches, 1)
-        overlapped_launch_s = kern_ms / 1e3 / max(launches, 1)
-        alg_bytes = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] +
-                     B_HIT * cst["hits"] + B_PIX * P)
-        per_launch = alg_bytes / max(launches / a.steps, 1)
-        achieved = per_launch / avg_launch_s / 1e9
+        img_sha1 = frame_sha1(img)
+        assert img_sha1 == count_sha1, "the timed frame differs from the counting frame"
+        # ---- roofline of the dominant kernel.  The timed frames run two
+        # pass sets on two HIP streams, so their kernels overlap and no
+        # kernel's duration is its own.  One more frame (after the timed
+        # region) runs the same passes on ONE stream with HIP events around
+        # every launch: exclusive per-kernel durations (what the committed
+        # rocprofv3 profile of `bench.py --one-set` reports).
+        rres = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world, packed=True,
+                                 flags=native.FLAG_ONE_SET | native.FLAG_KERNEL_TIMES)
+        rprof = rs.context.profile()
+        if world == 1:
+            assert frame_sha1(rres["packed"]) == img_sha1, "the one-stream frame differs"
+        else:   # this rank's tiles only (no collective here: the other ranks wait at the barrier)
+            assert rres["stats"]["segments"] == cst["segments"]
+        kt = rprof["kernels"]
+        dom = max(kt, key=lambda k: kt[k]["ms"])
+        dom_name = {"primary": "wf_kernel (primary)", "park": "wf_park_kernel", "shade": "wf_shade_kernel",
+                    "bounce": "wf_kernel (bounce)", "resolve": "wf_resolve_kernel"}[dom]
+        launch_s = kt[dom]["ms"] / 1e3 / kt[dom]["launches"]
+        # algorithmic work of the dominant kernel's launches:
+        # the park kernel traces the bounce segments = all - primary
+        pc = cprof["primary"]
+        if dom == "park":
+            cells = cst["cells_visited"] - pc["cells_visited"]
+            tests = cst["triangle_tests"] - pc["triangle_tests"]
+            alg = B_CELL * cells + B_TRI * tests
+        else:
+            alg = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] + B_HIT * cst["hits"] + B_PIX * P)
+        alg_per_launch = alg / kt[dom]["launches"]
+        roof = {"bound": "issue", "kernel": dom_name,
+                "launch_ms": round(launch_s * 1e3, 3), "launches_per_frame": kt[dom]["launches"],
+                "launch_time": "exclusive: HIP events around each launch of one extra frame whose passes "
+                               "run on one stream (the timed frames overlap two streams)",
+                "per_kernel_ms_one_stream": {k: round(v["ms"], 3) for k, v in kt.items()},
+                "limiter": "VALU issue in the walk, dependent-load latency in the test rounds; "
+                           "not DRAM bandwidth (memory_side below)",
+                "achieved": None, "peak": round(PEAK_VALU_GLANE, 1), "unit": "Glane-op/s", "frac": None,
+                "traffic": None}
+        rp = roofline_profile_for(a.config) if spp == cfgd["spp"] and world == 1 else None
+        if rp:
+            d, src = rp
+            kk = d["kernels"].get({"park": "wf_park_kernel", "shade": "wf_shade_kernel"}.get(dom, dom_name))
+            if kk:
+                lane_ops = kk["valu_insts_per_launch"] * 64 * kk["lane_util"]
+                roof["achieved"] = round(lane_ops / launch_s / 1e9, 1)
+                roof["frac"] = round(roof["achieved"] / PEAK_VALU_GLANE, 4)
+                roof["lane_ops_per_launch"] = lane_ops
+                roof["profile"] = src
+                roof["profile_launch_ms"] = kk.get("avg_ms")
+                roof["profile_valu_issue_frac"] = kk.get("valu_issue_frac")
+                roof["profile_lane_util"] = kk.get("lane_util")
+                if kk.get("hbm_bytes_per_launch"):
+                    tb = kk["hbm_bytes_per_launch"]
+                    roof["traffic"] = round(tb / 1e9, 3)
+                    roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections)"
+                    roof["memory_side"] = {"achieved": round(tb / launch_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                           "unit": "GB/s", "frac": round(tb / launch_s / 1e9 / PEAK_HBM_GBS, 4)}
+        roof["algorithmic"] = {
+            "what": "SURVEY.md d4 bytes of the kernel's work (8 B per visited cell, 36 B per triangle test"
+                    + ("" if dom == "park" else ", hit data + texels, 3 B per pixel") +
+                    ") per second: a work rate in HBM-equivalent bytes, NOT DRAM traffic (empty cells are "
+                    "answered from LDS, re-reads hit L2)",
+            "GB_per_launch": round(alg_per_launch / 1e9, 3),
+            "achieved": round(alg_per_launch / launch_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(alg_per_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4)}
+        # the whole frame's d4 rate over the timed (two-stream) frames: round
+        # 2's figure, kept for continuity
+        frame_alg = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] + B_HIT * cst["hits"] + B_PIX * P)
+        roof["frame_algorithmic"] = {"GB_per_frame": round(frame_alg / 1e9, 1),
+                                     "GBps": round(frame_alg * a.steps / (gpu_ms / 1e3) / 1e9, 1),
+                                     "frac": round(frame_alg * a.steps / (gpu_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                                     "gpu_ms_per_step": round(gpu_ms / a.steps, 3),
+                                     "avg_launch_ms_overlapped": round(kern_ms / max(launches, 1), 3)}
         out = {
             "metric": "Mrays/sec + wall-clock to output.png on contest config.json scene",
             "value": round(total_segs / elapsed / 1e6, 3),
@@ -333,46 +440,27 @@ def main():
                                    f"{cam.w}x{cam.h}, {spp} spp, max_bounce "
                                    f"{cfgd['max_bounce']}, grid 128^3",
                        "global_batch": cam.w * cam.h * spp, "parallelism": f"tiles{world}",
-                       "segments_per_step": int(total_segs / a.steps)},
-            # the roofline contract names hbm|mfma; this kernel is a pointer
-            # chase: its achieved fraction is algorithmic bytes over launch
-            # time, and the memory side (PMC bytes over launch time) is far
-            # lower -- it is bound by the latency of dependent loads under
-            # divergence, not by DRAM bandwidth (profiles/)
-            "roofline": {"bound": "hbm", "limiter": "latency", "achieved": round(achieved, 1),
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                         "traffic": None,
-                         "kernel": "trace launches: wf_kernel<7,true> (primary), wf_park_kernel + "
-                                   "wf_shade_kernel (each bounce)",
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                         "avg_launch_ms_overlapped": round(overlapped_launch_s * 1e3, 3),
-                         "gpu_ms_per_step": round(gpu_ms / a.steps, 3),
-                         "launch_time": "step GPU time / launches: two passes run at once on two "
-                                        "HIP streams, so launches overlap; avg_launch_ms_overlapped "
-                                        "is the per-launch HIP-event interval (rocprofv3's durations)",
-                         "alg_GB_per_launch": round(per_launch / 1e9, 3)},
+                       "segments_per_step": int(total_segs / a.steps),
+                       "schedule": "one pass set (profiling)" if a.one_set else
+                                   f"{cprof['passes']} counting passes; timed: default pass sets"},
+            "img_sha1": img_sha1,
+            "roofline": roof,
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},
+            "work_primary": pc,
             # SURVEY.md d1's companion rate: w*h*spp per second of the timed frames
             "msamples_per_s": round(cam.w * cam.h * spp * a.steps / elapsed / 1e6, 3),
         }
-        vc = valu_for(a.config) if spp == cfgd["spp"] else None
-        if vc:
-            out["roofline"]["valu_issue"] = vc
-        tr = traffic_for(a.config, "wf_shade_kernel") if spp == cfgd["spp"] else None
-        if tr:
-            mem_gbs = tr[0] / 1e9 / avg_launch_s
-            out["roofline"]["traffic"] = round(tr[0] / 1e9, 3)
-            out["roofline"]["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
-            out["roofline"]["traffic_source"] = tr[1]
-            out["roofline"]["memory_side_GBps"] = round(mem_gbs, 1)
-            out["roofline"]["frac_memory_side"] = round(mem_gbs / PEAK_HBM_GBS, 4)
+        if world > 1:
+            out["backend"] = a.backend
         if world == 1 and not a.no_wall_clock:
             out.update(wall_clock(soup, cfgd, cpu=not a.no_cpu_baseline))
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(soup, cfgd, a.cpu_seconds)
             out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
     rs.close()
     if world > 1:
         dist.destroy_process_group()

@@ -113,6 +113,11 @@ typedef struct zrt_render_config {
 #define ZRT_FLAG_COUNT_STATS  0x1u   /* count cells/tests/hits (slower kernel variant) */
 #define ZRT_FLAG_LANE_WALK    0x2u   /* every launch walks + tests per lane (no park kernel) */
 /* 0x4, 0x8: reserved (round-2 kernel variants that were measured slower and removed) */
+#define ZRT_FLAG_ONE_SET      0x10u  /* every pass on the context's one stream (no second pass set, no
+                                        lead): kernels never overlap, so their durations are exclusive
+                                        (the roofline measurement); same image */
+#define ZRT_FLAG_KERNEL_TIMES 0x20u  /* HIP events around every kernel launch: per-kernel device times
+                                        in zrt_context_profile (adds ~10 us per launch) */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */
@@ -195,6 +200,31 @@ int zrt_context_create_built(const float* positions, const float* normals, const
 int zrt_context_render(zrt_context* ctx, const zrt_camera* camera, const zrt_render_config* cfg,
                        const zrt_outputs* outputs, zrt_stats* stats);
 void zrt_context_destroy(zrt_context* ctx);
+
+/* Per-kernel breakdown of the context's last zrt_context_render (bench.py's
+ * roofline: the dominant kernel's launch time and algorithmic work).
+ * ms / launches per kernel class; ms only with ZRT_FLAG_KERNEL_TIMES (else 0).
+ * primary_counts: segments, cells visited, triangle tests, hits of the
+ * primary (camera) segments, counting renders (ZRT_FLAG_COUNT_STATS) only --
+ * the bounce launches' work is zrt_stats' totals minus these. */
+enum {
+    ZRT_KERNEL_PRIMARY = 0,   /* wf_kernel, primary launch (camera rays) */
+    ZRT_KERNEL_PARK = 1,      /* wf_park_kernel, bounce trace */
+    ZRT_KERNEL_SHADE = 2,     /* wf_shade_kernel, bounce shading */
+    ZRT_KERNEL_BOUNCE = 3,    /* wf_kernel, bounce launch (lane walk / no OccX) */
+    ZRT_KERNEL_RESOLVE = 4,   /* wf_resolve_kernel / resolve_kernel */
+    ZRT_KERNEL_COUNT = 5,     /* trace_kernel (counting build) */
+    ZRT_KERNEL_CLASSES = 8
+};
+typedef struct zrt_kernel_profile {
+    double ms[ZRT_KERNEL_CLASSES];
+    uint32_t launches[ZRT_KERNEL_CLASSES];
+    uint32_t passes;                 /* passes of the frame */
+    uint32_t sets;                   /* pass sets (streams) it ran on */
+    uint64_t primary_counts[4];
+} zrt_kernel_profile;
+int zrt_context_profile(const zrt_context* ctx, zrt_kernel_profile* out);
+
 /* The context's grid and {num_refs, empty cells, min refs of a non-empty cell
  * (0xFFFFFFFF if none), max refs of a cell}: the grid statistics the
  * reference logs after Geometry.build (main.zig:117-118), without a host copy

@@ -127,3 +127,34 @@ def test_two_ranks_on_one_gpu_gather_gloo(tmp_path):
     for p in procs:
         assert p.wait(timeout=300) == 0
     assert np.array_equal(np.load(out), ref)
+
+
+def _bench_json(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, stdout[-2000:]
+    import json
+    return json.loads(lines[0])
+
+
+def test_bench_entry_two_ranks_gloo_matches_one():
+    """bench.py's own N > 1 entry, end to end, as the driver launches it
+    (torch.distributed.run, one process per rank, rank 0 prints ONE line):
+    two gloo ranks sharing device 0 (--backend gloo is test-only; the driver's
+    8-GPU run uses RCCL).  The line says n_gpus 2 and its img_sha1 (the whole
+    gathered frame) equals the N = 1 run's."""
+    common = ["--config", "cfg2", "--spp", "4", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+              "--no-wall-clock"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + common, cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert one.returncode == 0, one.stderr[-3000:]
+    j1 = _bench_json(one.stdout)
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo"] + common,
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert two.returncode == 0, two.stderr[-3000:]
+    j2 = _bench_json(two.stdout)
+    assert j1["n_gpus"] == 1 and j2["n_gpus"] == 2
+    assert j1["img_sha1"] and j2["img_sha1"] == j1["img_sha1"]
+    assert j2["config"]["segments_per_step"] == j1["config"]["segments_per_step"]

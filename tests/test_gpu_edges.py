@@ -11,7 +11,10 @@ upload, and the device build straight into the context):
   build (linalg.zig:516-563);
 - a one-triangle scene, grid resolutions 1x1x1 and non-cubic, and grids
   large enough for coarser occupancy bricks (300x260x280, 640x256x512);
-- max_bounce 0 (primary rays only).
+- max_bounce 0 (primary rays only);
+- grids with an axis above 1024 cells (the unpacked walk);
+- the capacity guard's premise: counting, timed and counting renders on one
+  context at growing sizes (every buffer regrown before its launch).
 """
 import dataclasses
 import math
@@ -83,7 +86,11 @@ CASES = [("sphere", 1, 1, 3, 4, (128, 128, 128)),
          # grids whose 4^3-brick bits exceed wf_kernel's LDS share: coarser
          # occupancy bricks (8^3, 16^3), and no OccX (the lane-walk fallback)
          ("cornell_inside", 48, 40, 2, 4, (300, 260, 280)),
-         ("sphere", 32, 24, 1, 3, (640, 256, 512))]
+         ("sphere", 32, 24, 1, 3, (640, 256, 512)),
+         # an axis above 1024 cells: the unpacked ("wide") wf_kernel
+         # instantiations for the primary and the bounce launches
+         ("sphere", 40, 32, 2, 4, (1100, 8, 8)),
+         ("cornell_inside", 40, 32, 2, 4, (12, 1030, 9))]
 
 
 @pytest.fixture(scope="module")
@@ -120,3 +127,25 @@ def test_edge_render_bitexact_vs_oracle(oracle_mod, soups, name, w, h, spp, mb, 
         tuple(int(x) for x in ctr[:4])
     if name == "sky_only":   # the walk still runs: the box behind the camera is entered
         assert st["hits"] == 0
+
+
+def test_growing_frames_counting_timed_counting(oracle_mod):
+    """Round 2 once rendered a counting frame through a d_out that the timed
+    path had never allocated.  One fresh context, frames of growing size,
+    alternating counting (trace_kernel) and timed (wavefront) renders: every
+    one equals the oracle, so every buffer was regrown before its launch
+    (zrt_context_render checks each one's capacity before launching)."""
+    soup = scenes.get_scene("cornell")
+    c = soup.camera(None)
+    rs = RenderScene(soup)
+    osc = oracle_mod.OracleScene(soup)
+    try:
+        for w, h, spp in ((16, 16, 1), (48, 40, 3), (96, 64, 5), (160, 120, 2)):
+            cam = camera_for(soup, None, w, h)
+            ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
+            rgb, _, _ = osc.render(ocam, spp, 4, oracle_mod.RNG_PATH, 0, 16, want_linear=False)
+            for counting in (True, False, True):
+                img, _ = rs.render(cam, num_samples=spp, max_bounce=4, stats=counting)
+                assert np.array_equal(img.reshape(-1, 3), rgb), (w, h, spp, counting)
+    finally:
+        rs.close()

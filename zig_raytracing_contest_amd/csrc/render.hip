@@ -321,6 +321,7 @@ __global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams
 
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t n_seg = 0, n_cells = 0, n_tests = 0, n_hits = 0;
+    uint32_t p_seg = 0, p_cells = 0, p_tests = 0, p_hits = 0;   // the primary (camera) segments' share
 
     for (;;) {
         uint32_t base = 0;
@@ -341,10 +342,13 @@ __global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams
             ++n_seg;
             float hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
+            const uint32_t c_before = n_cells, t_before = n_tests;
             const float t = trace_ray<true, kTriBatch>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof,
                                                        s_wcnt);
+            if (slot == 0) { ++p_seg; p_cells += n_cells - c_before; p_tests += n_tests - t_before; }
             if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
             ++n_hits;
+            if (slot == 0) ++p_hits;
             // stage3.zig:199-206
             const float4* tdp = p.tri_data + 4ull * hidx;
             const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
@@ -375,7 +379,13 @@ __global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams
                              s3 = wave_sum(n_hits), s4 = wave_sum(prof[6]), s5 = wave_sum(prof[7]),
                              s6 = wave_sum(prof[8]), s7 = wave_sum(prof[9]), s8 = wave_sum(prof[10]),
                              s9 = wave_sum(prof[4]);
+    const unsigned long long q0 = wave_sum(p_seg), q1 = wave_sum(p_cells), q2 = wave_sum(p_tests),
+                             q3 = wave_sum(p_hits);
     if (lane == 0) {
+        atomicAdd(&p.stats[8], q0);
+        atomicAdd(&p.stats[9], q1);
+        atomicAdd(&p.stats[10], q2);
+        atomicAdd(&p.stats[11], q3);
         atomicAdd(&p.stats[0], s0);
         atomicAdd(&p.stats[1], s1);
         atomicAdd(&p.stats[2], s2);
@@ -1290,6 +1300,10 @@ struct zrt_context {
     uint32_t* d_counter = nullptr;
     unsigned long long* d_stats = nullptr;
     int num_cus = 0;
+    // ZRT_FLAG_KERNEL_TIMES: an event pair per kernel launch and its class
+    std::vector<hipEvent_t> ev_k;
+    std::vector<uint8_t> ev_k_cls;
+    zrt_kernel_profile prof{};         // of the last render (zrt_context_profile)
     // cached pixel list
     std::vector<uint32_t> pix;
     uint32_t pix_key[5] = {0, 0, 0, 0, 0};
@@ -1387,6 +1401,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     }
     for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_pass) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_k) (void)hipEventDestroy(e);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
     if (c->ev_end) (void)hipEventDestroy(c->ev_end);
@@ -1466,6 +1481,12 @@ static int context_base(zrt_context* c) {
 
 static int context_materials(zrt_context* c, const zrt_scene* s);
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells);
+
+static int context_counters(zrt_context* c) {
+    HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
+    HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
+    return ZRT_OK;
+}
 
 static int context_init(zrt_context* c, const zrt_scene* s) {
     int rc = context_base(c);
@@ -1556,11 +1577,27 @@ __global__ __launch_bounds__(kBlock) void occ_coarsen_kernel(const uint32_t* __r
     atomicOr(&out[cb >> 5], 1u << (cb & 31u));
 }
 
+// Coarse brick bits straight from the cells (device-built grids whose 4^3
+// bricks are too many for OccX): one thread per cell, atomicOr per non-empty one.
+__global__ __launch_bounds__(kBlock) void occ_cells_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                           uint32_t ncells, uint32_t sh, uint32_t cn0, uint32_t cn01,
+                                                           uint32_t* __restrict__ out) {
+    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint2 c = cells[ci];
+        if (c.x >= c.y) continue;
+        const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / r0 / r1;
+        const uint32_t cb = (z >> sh) * cn01 + (y >> sh) * cn0 + (x >> sh);
+        atomicOr(&out[cb >> 5], 1u << (cb & 31u));
+    }
+}
+
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     const uint32_t* r = c->grid.resolution;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
     const uint64_t nb = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
-    if (nb > (1ull << 24)) return ZRT_ERR_UNSUPPORTED;    // brick indices are 24-bit (__umul24)
+    // more than 2^24 4^3 bricks (> 2^30 cells): no OccX (24-bit brick
+    // indices), the bounces take the lane walk over the coarse bits below
+    const bool occx_possible = occx_usable(nb, 0, 0, 1);
     const uint64_t nbw = (nb + 31) / 32;
     uint32_t sh = 2;
     auto words_at = [&](uint32_t k) {
@@ -1574,7 +1611,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     c->occ_words = (uint32_t)words_at(sh);
     HIP_TRY(hipMalloc((void**)&c->d_occ, 4ull * c->occ_words));
     if (host_cells) {
-        std::vector<unsigned long long> mask(nb, 0ull);
+        std::vector<unsigned long long> mask(occx_possible ? nb : 0, 0ull);
         std::vector<uint32_t> coarse(c->occ_words, 0u);
         for (uint32_t z = 0; z < r[2]; ++z)
             for (uint32_t y = 0; y < r[1]; ++y)
@@ -1582,11 +1619,16 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                     const uint64_t ci = ((uint64_t)z * r[1] + y) * r[0] + x;
                     if (host_cells[2 * ci] < host_cells[2 * ci + 1]) {
                         const uint64_t b = ((uint64_t)(z >> 2) * c->occx_nb[1] + (y >> 2)) * c->occx_nb[0] + (x >> 2);
-                        mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
+                        if (occx_possible) mask[b] |= 1ull << (((z & 3u) << 4) | ((y & 3u) << 2) | (x & 3u));
                         const uint64_t cb = ((uint64_t)(z >> sh) * c->occ_nb[1] + (y >> sh)) * c->occ_nb[0] + (x >> sh);
                         coarse[cb >> 5] |= 1u << (cb & 31);
                     }
                 }
+        HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
+        if (!occx_possible) {
+            c->occx_ok = false;
+            return context_counters(c);
+        }
         std::vector<uint32_t> bits(nbw, 0u);
         std::vector<uint16_t> prefix(nbw, 0);
         std::vector<unsigned long long> masks;
@@ -1597,10 +1639,9 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                 if (mask[b]) { bits[wd] |= 1u << (b & 31); masks.push_back(mask[b]); ++run; }
         }
         masks.push_back(0ull);
-        HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
         uint64_t moff, words;
         occx_layout(nbw, run, &moff, &words);
-        c->occx_ok = run < 0xFFFF && occx_lds_words(nbw, moff, words) * 4 <= kOccxBudget;
+        c->occx_ok = occx_usable(nb, run, occx_lds_words(nbw, moff, words) * 4, kOccxBudget);
         if (c->occx_ok) {
             std::vector<uint32_t> blob(words, 0u);
             memcpy(blob.data(), bits.data(), nbw * 4);
@@ -1612,17 +1653,34 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
             HIP_TRY(hipMalloc((void**)&c->d_occx, words * 4));
             HIP_TRY(hipMemcpy(c->d_occx, blob.data(), words * 4, hipMemcpyHostToDevice));
         }
+    } else if (!occx_possible) {
+        HIP_TRY(hipMemsetAsync(c->d_occ, 0, 4ull * c->occ_words, c->stream));
+        hipLaunchKernelGGL(occ_cells_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells,
+                           sh, c->occ_nb[0], c->occ_nb[0] * c->occ_nb[1], c->d_occ);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        c->occx_ok = false;
     } else {
         // the blob for the largest possible occupancy, then the real size
         uint64_t moff, words;
         occx_layout(nbw, nb, &moff, &words);
-        unsigned long long* d_masks = nullptr;
+        // the scratch buffers are freed on every exit path (the blob belongs
+        // to the context as soon as it exists)
+        struct Scratch {
+            unsigned long long* masks = nullptr;
+            uint32_t* n = nullptr;
+            ~Scratch() {
+                if (masks) (void)hipFree(masks);
+                if (n) (void)hipFree(n);
+            }
+        } tmp;
         uint32_t* d_blob = nullptr;
-        uint32_t* d_n = nullptr;
-        HIP_TRY(hipMalloc((void**)&d_masks, nb * 8));
+        HIP_TRY(hipMalloc((void**)&tmp.masks, nb * 8));
+        HIP_TRY(hipMalloc((void**)&tmp.n, 4));
         HIP_TRY(hipMalloc((void**)&d_blob, words * 4));
-        HIP_TRY(hipMalloc((void**)&d_n, 4));
         c->d_occx = d_blob;            // freed with the context from here on
+        unsigned long long* const d_masks = tmp.masks;
+        uint32_t* const d_n = tmp.n;
         HIP_TRY(hipMemsetAsync(d_blob, 0, words * 4, c->stream));
         hipLaunchKernelGGL(occx_mask_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                            c->d_cells, r[0], r[1], r[2], c->occx_nb[0], c->occx_nb[1], (uint32_t)nb, d_masks, d_blob);
@@ -1643,18 +1701,14 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         uint32_t run = 0;
         HIP_TRY(hipMemcpyAsync(&run, d_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        (void)hipFree(d_masks);
-        (void)hipFree(d_n);
         HIP_TRY(le);
         occx_layout(nbw, run, &moff, &words);
-        c->occx_ok = run < 0xFFFF && occx_lds_words(nbw, moff, words) * 4 <= kOccxBudget;
+        c->occx_ok = occx_usable(nb, run, occx_lds_words(nbw, moff, words) * 4, kOccxBudget);
         c->occx_words = (uint32_t)words;
         c->occx_nbw = (uint32_t)nbw;
         c->occx_moff = (uint32_t)moff;
     }
-    HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
-    HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
-    return ZRT_OK;
+    return context_counters(c);
 }
 
 extern "C" int zrt_context_create(const zrt_scene* s, int device, zrt_context** out) {
@@ -1852,6 +1906,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_SETS")) want_sets = (uint32_t)std::max(1, std::min((int)kMaxPassSets, atoi(e)));
 #endif
+    const bool ktimes = (cfg->flags & ZRT_FLAG_KERNEL_TIMES) != 0;
     size_t held = 16ull * c->out_cap;
     for (const zrt_context::PassSet& ps : c->set)
         held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk_cap + ps.hit_cap) + 4ull * ps.wfc_cap;
@@ -1862,13 +1917,18 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // drain (tails, the latency-bound shade kernel beside the park kernel):
     // two sets cfg3 -5%, cfg2 -9%, cfg5 -7% frame time, images identical
     // (r02c1, profiles/r02/r02c1_ab_two_streams.log)
-    const uint32_t nsets = counting ? 1u : std::min<uint32_t>(npasses, want_sets);
+    const uint32_t plan_sets = counting ? 1u : std::min<uint32_t>(npasses, want_sets);
+    // ZRT_FLAG_ONE_SET: the same passes (split and lead as planned for the
+    // sets) run one after another on the context's stream, so no kernel
+    // overlaps another: exclusive kernel durations for bench.py's roofline,
+    // the same per-launch work as the frame it stands for
+    const uint32_t nsets = (cfg->flags & ZRT_FLAG_ONE_SET) ? 1u : plan_sets;
     // lead: samples moved from the last pass to the first.  The second set's
     // first primary launch waits for the first's (it fills every CU), so the
     // second set ends behind the first unless the first has more work.
-    uint32_t lead_pct = nsets > 1 ? kLeadPct : 0u;
+    uint32_t lead_pct = plan_sets > 1 ? kLeadPct : 0u;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
-    if (const char* e = getenv("ZRT_LEAD")) lead_pct = nsets > 1 ? (uint32_t)std::max(0, std::min(50, atoi(e))) : 0u;
+    if (const char* e = getenv("ZRT_LEAD")) lead_pct = plan_sets > 1 ? (uint32_t)std::max(0, std::min(50, atoi(e))) : 0u;
 #endif
     const uint64_t last_n = spp - (uint64_t)(npasses - 1) * s_pass;     // samples of the last pass
     const uint64_t cap_items = std::max<uint64_t>(1, 0x7FFFFF00ull / P);
@@ -1916,6 +1976,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         c->ev_trace.push_back(e);
     }
 
+    // per-kernel events: per pass the primary, nb - 1 bounces of up to two
+    // kernels, the resolve
+    const size_t nk = ktimes ? (size_t)npasses * (2 * nb + 1) : 0;
+    while (c->ev_k.size() < 2 * nk) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->ev_k.push_back(e);
+    }
+    c->ev_k_cls.assign(nk, 0);
+
     // Kernel per launch: the park kernel (traces, writes hit records) +
     // wf_shade_kernel for the bounce launches (incoherent rays) when the
     // scene's OccX fits the LDS budget, wf_kernel for the primary launch
@@ -1938,6 +2008,37 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const WfFn s_next = (WfFn)wf_shade_kernel;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
         if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
+
+    // Capacity guard: every buffer a launch below writes holds what that
+    // launch writes (round 2's counting render once wrote through an
+    // unallocated d_out after a refactor of the pass logic; a stale, smaller
+    // buffer must not pass silently either).  Queues 3 float4 per item, bounce
+    // planes 2 per (slot, item), terminal radiance / hit records / counting
+    // output 1 per item, the pass's items S * P <= T (checked per pass).
+    {
+        auto shortfall = [&](const char* what, const void* ptr, size_t cap, uint64_t need) {
+            if (ptr && cap >= need) return false;
+            if (getenv("ZRT_DEBUG"))
+                fprintf(stderr, "zrt: capacity guard: %s holds %zu, the launch writes %llu\n", what, ptr ? cap : 0,
+                        (unsigned long long)need);
+            return true;
+        };
+        bool bad = shortfall("pixel list", c->d_pix, c->pix_cap, P) || shortfall("rgb", c->d_rgb, c->rgb_cap, 3ull * P) ||
+                   (npasses > 1 && shortfall("accumulator", c->d_acc, c->acc_cap, P)) ||
+                   (want_lin && shortfall("linear", c->d_lin, c->lin_cap, 3ull * P)) ||
+                   (counting && shortfall("counting output", c->d_out, c->out_cap, T));
+        for (uint32_t k = 0; k < nsets && !counting && !bad; ++k) {
+            const zrt_context::PassSet& ps = c->set[k];
+            bad = shortfall("q0", ps.q0, ps.q0_cap, 3 * T) || shortfall("q1", ps.q1, ps.q1_cap, 3 * T) ||
+                  shortfall("term", ps.term, ps.term_cap, T) || shortfall("planes", ps.stk, ps.stk_cap, 2 * T * nb) ||
+                  shortfall("counters", ps.wfc, ps.wfc_cap, 24ull * kCtr * (mb + 2)) ||
+                  (park_next && shortfall("hit records", ps.hit, ps.hit_cap, T)) ||
+                  (k > 0 && (!ps.stream || !ps.ev_join));
+        }
+        for (uint32_t pass = 0; pass < npasses && !bad; ++pass)
+            bad = (uint64_t)pass_count(pass) * P > T || pass_first(pass) + pass_count(pass) > spp;
+        if (bad) return ZRT_ERR_INVALID_ARG;
+    }
 
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
@@ -2003,6 +2104,20 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.stats = c->d_stats;
     // stage3.zig:223 inv_num_samples = ones / splat(spp)  (f32 division)
     const float inv_spp = 1.0f / (float)spp;
+    size_t kn = 0;                             // kernels launched (ZRT_FLAG_KERNEL_TIMES)
+    auto kt_begin = [&](int cls, hipStream_t sm) -> int {
+        if (!ktimes) return ZRT_OK;
+        c->ev_k_cls[kn] = (uint8_t)cls;
+        HIP_TRY(hipEventRecord(c->ev_k[2 * kn], sm));
+        return ZRT_OK;
+    };
+    auto kt_end = [&](hipStream_t sm) -> int {
+        if (!ktimes) return ZRT_OK;
+        HIP_TRY(hipEventRecord(c->ev_k[2 * kn + 1], sm));
+        ++kn;
+        return ZRT_OK;
+    };
+    zrt_kernel_profile kp{};
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
@@ -2054,34 +2169,50 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.hit = hit;
                 W.fetch8s = wfc + kCtr * (16 * (mb + 2) + 8 * k);
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
+                const int cls = k == 0 ? ZRT_KERNEL_PRIMARY : (park_next ? ZRT_KERNEL_PARK : ZRT_KERNEL_BOUNCE);
+                if ((rc = kt_begin(cls, sm)) != ZRT_OK) return rc;
                 if (k == 0)
                     hipLaunchKernelGGL(f_first, dim3(grid_first), dim3(thr_first), lds_first, sm, W);
                 else
                     hipLaunchKernelGGL(f_next, dim3(grid_next), dim3(thr_next), lds_next, sm, W);
                 HIP_TRY(hipGetLastError());
+                if ((rc = kt_end(sm)) != ZRT_OK) return rc;
+                ++kp.launches[cls];
                 if (k > 0 && park_next) {                    // same bounce, shading half
+                    if ((rc = kt_begin(ZRT_KERNEL_SHADE, sm)) != ZRT_OK) return rc;
                     hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), 0, sm, W);
                     HIP_TRY(hipGetLastError());
+                    if ((rc = kt_end(sm)) != ZRT_OK) return rc;
+                    ++kp.launches[ZRT_KERNEL_SHADE];
                 }
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 ++launches;
             }
             // the passes' sums into acc stay in pass order (stage3.zig:236-242)
             if (nsets > 1 && pass > 0) HIP_TRY(hipStreamWaitEvent(sm, c->ev_pass[pass - 1], 0));
+            if ((rc = kt_begin(ZRT_KERNEL_RESOLVE, sm)) != ZRT_OK) return rc;
             hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, sm,
                                term, stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
                                c->d_rgb, want_lin ? c->d_lin : nullptr);
+            if ((rc = kt_end(sm)) != ZRT_OK) return rc;
+            ++kp.launches[ZRT_KERNEL_RESOLVE];
             if (nsets > 1) HIP_TRY(hipEventRecord(c->ev_pass[pass], sm));
         } else {
             HIP_TRY(hipMemsetAsync(c->d_counter, 0, 4, c->stream));
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+            if ((rc = kt_begin(ZRT_KERNEL_COUNT, c->stream)) != ZRT_OK) return rc;
             hipLaunchKernelGGL(cfn, dim3(grid_count), dim3(kTraceThreads), lds_wf, c->stream, tp);
             HIP_TRY(hipGetLastError());
+            if ((rc = kt_end(c->stream)) != ZRT_OK) return rc;
+            ++kp.launches[ZRT_KERNEL_COUNT];
             ++launches;
             HIP_TRY(hipEventRecord(c->ev_trace[ne++], c->stream));
+            if ((rc = kt_begin(ZRT_KERNEL_RESOLVE, c->stream)) != ZRT_OK) return rc;
             hipLaunchKernelGGL(resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
                                c->d_out, P, S, c->d_acc, first, last, inv_spp, c->d_rgb,
                                want_lin ? c->d_lin : nullptr);
+            if ((rc = kt_end(c->stream)) != ZRT_OK) return rc;
+            ++kp.launches[ZRT_KERNEL_RESOLVE];
         }
         HIP_TRY(hipGetLastError());
     }
@@ -2123,6 +2254,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if (wf_debug) fprintf(stderr, "{\"zrt_launch\": %u, \"ms\": %.3f}\n", e / 2, t);
     }
     st.trace_launches = launches;
+    for (size_t k = 0; k < kn; ++k) {
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, c->ev_k[2 * k], c->ev_k[2 * k + 1]));
+        kp.ms[c->ev_k_cls[k]] += t;
+    }
+    kp.passes = npasses;
+    kp.sets = counting ? 1u : nsets;
+    if (counting)
+        for (int k = 0; k < 4; ++k) kp.primary_counts[k] = hs[8 + k];
+    c->prof = kp;
     st.segments = hs[0];
     st.cells_visited = hs[1];
     st.triangle_tests = hs[2];
@@ -2140,6 +2281,12 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (want_lin)
         HIP_TRY(hipMemcpy(outs->linear_packed, c->d_lin, 3ull * P * sizeof(float), hipMemcpyDeviceToHost));
     if (stats) *stats = st;
+    return ZRT_OK;
+}
+
+extern "C" int zrt_context_profile(const zrt_context* c, zrt_kernel_profile* out) {
+    if (!c || !out) return ZRT_ERR_INVALID_ARG;
+    *out = c->prof;
     return ZRT_OK;
 }
 

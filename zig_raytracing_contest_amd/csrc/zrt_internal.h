@@ -24,6 +24,17 @@ void zig_tables(double zx[257], double zf[257]);
 // when set (the per-GPU CPU share on shared GPU hosts).
 unsigned host_threads();
 
+// Whether the park kernel's exact per-cell occupancy (OccX) serves a grid:
+// its 4^3-cell bricks need 24-bit indices (__umul24 in the kernels), the
+// occupied-brick count before a 32-brick word must fit the u16 prefix, and
+// the blob must fit the LDS left beside the per-wave slots.  Otherwise the
+// bounces take the lane walk (wf_kernel, coarsened brick bits): the render
+// still runs, on every grid the reference accepts (u32 resolution, < 2^31
+// cells), with the same image.
+inline bool occx_usable(uint64_t bricks, uint64_t occupied, uint64_t lds_bytes, uint64_t budget) {
+    return bricks <= (1ull << 24) && occupied < 0xFFFFull && lds_bytes <= budget;
+}
+
 // Host-side packed pixel order of one rank (zrt_tile_pixels).
 int tile_pixels(uint32_t w, uint32_t h, uint32_t tile, uint32_t rank, uint32_t nranks,
                 uint32_t* out, uint32_t* count);

@@ -20,6 +20,9 @@ STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime
           -4: "out of memory", -5: "unsupported configuration", -6: "I/O error",
           -7: "parse error", -8: "not found", -9: "camera/output size rules violated"}
 FLAG_COUNT_STATS, FLAG_LANE_WALK = 0x1, 0x2
+FLAG_ONE_SET, FLAG_KERNEL_TIMES = 0x10, 0x20
+# zrt_kernel_profile classes (include/zrt.h)
+KERNEL_CLASSES = ("primary", "park", "shade", "bounce", "resolve", "count")
 
 PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
@@ -84,6 +87,18 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
 
 
+class KernelProfile(C.Structure):
+    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_uint32 * 8), ("passes", C.c_uint32),
+                ("sets", C.c_uint32), ("primary_counts", C.c_uint64 * 4)]
+
+    def as_dict(self):
+        return {"kernels": {k: {"ms": self.ms[i], "launches": int(self.launches[i])}
+                            for i, k in enumerate(KERNEL_CLASSES) if self.launches[i]},
+                "passes": int(self.passes), "sets": int(self.sets),
+                "primary": dict(zip(("segments", "cells_visited", "triangle_tests", "hits"),
+                                    (int(x) for x in self.primary_counts)))}
+
+
 class Outputs(C.Structure):
     _fields_ = [("rgb_image", C.c_void_p), ("rgb_packed", C.c_void_p),
                 ("linear_packed", C.c_void_p), ("device_rgb_packed", C.c_void_p)]
@@ -95,7 +110,7 @@ EXPORTS = [
     "zrt_geometry_scene", "zrt_geometry_indices", "zrt_geometry_free", "zrt_render",
     "zrt_context_create", "zrt_context_create_built", "zrt_context_grid_info", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
     "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
-    "zrt_camera_from_matrix", "zrt_probe", "zrt_timed_kernels",
+    "zrt_camera_from_matrix", "zrt_probe", "zrt_timed_kernels", "zrt_context_profile",
 ]
 
 
@@ -129,6 +144,7 @@ def lib():
     L.zrt_context_grid_info.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
     L.zrt_context_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig),
                                      C.POINTER(Outputs), C.POINTER(Stats)]
+    L.zrt_context_profile.argtypes = [C.c_void_p, C.POINTER(KernelProfile)]
     L.zrt_context_destroy.argtypes = [C.c_void_p]
     L.zrt_context_destroy.restype = None
     L.zrt_tile_pixels.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -281,6 +297,14 @@ class Context:
         info = (C.c_uint32 * 4)()
         check(lib().zrt_context_grid_info(self._h, None, info), "zrt_context_grid_info")
         return tuple(int(x) for x in info)
+
+    def profile(self):
+        """zrt_context_profile: per-kernel launches (and device ms with
+        FLAG_KERNEL_TIMES) of the last render, primary-segment counts of a
+        counting render."""
+        kp = KernelProfile()
+        check(lib().zrt_context_profile(self._h, C.byref(kp)), "zrt_context_profile")
+        return kp.as_dict()
 
     def close(self):
         if getattr(self, "_h", None) is not None and _lib is not None:
