@@ -54,30 +54,43 @@ static std::vector<Rec> walk_cells(const TestGrid& g, const GridK& k, Dda s) {
 static uint64_t g_texit_fails = 0;
 static uint64_t g_walk_fails = 0, g_walk_steps = 0;
 
-// DDAW_STEP (the park kernel's walk) against DDA_STEP, step by step: cells,
-// linear index, crossing flag, T_EXIT and the next crossing ts bit for bit
-// and DDAP_STEP (the packed cell of the park walk) the same way: packed cell,
-// linear index, crossing flag, T_EXIT and ts bit for bit up to the exit step
-// (past it the packed fields may carry; the walk has ended there)
+// DDAW_STEP (the unpacked walk) against DDA_STEP, step by step: cells,
+// linear index, crossing flag, T_EXIT and the next crossing ts bit for bit;
+// and DDAV_STEPX (the packed walks, per-grid field widths) the same way: the
+// packed word equals the cell's packing (and, on power-of-two grids, the
+// linear index), the crossing flag, T_EXIT = EXITED ? +inf : TC and the ts bit
+// for bit up to the exit step (past it the packed fields may carry; the walk
+// has ended there), and the in-brick index of the park walk's OccX test.
 static void walk_w(const GridK& k, Dda s) {
     DdaW w;
     ddaw_from(s, k, w);
-    DdaP q;
-    ddap_from(s, k, q);
+    const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
+    PackK pk;
+    const bool packs = pack_layout(res, pk);
+    if (!packs) { ++g_walk_fails; return; }
+    const bool linear = pack_is_linear(res, pk);
+    DdaV x;
+    ddav_from(s, k, pk, x);
     for (int guard = 0; guard < 100000; ++guard) {
-        bool c1, c2, c3;
-        float e1, e2, e3;
+        bool c1, c2, c4, ex4;
+        float e1, e2, tc4;
         DDA_STEP(s, k, 2, c1, e1);
         DDAW_STEP(w, 2, c2, e2);
-        DDAP_STEP(q, kPackLow2, c3, e3);
+        DDAV_STEPX(x, pk, pk.low2, c4, ex4, tc4);
         ++g_walk_steps;
         const bool same = c1 == c2 && !memcmp(&e1, &e2, 4) && s.c0 == w.c0 && s.c1 == w.c1 && s.c2 == w.c2 &&
                           s.lin == w.lin && !memcmp(&s.tn0, &w.tn0, 4) && !memcmp(&s.tn1, &w.tn1, 4) &&
                           !memcmp(&s.tn2, &w.tn2, 4);
-        const bool same_p = !memcmp(&e1, &e3, 4) && s.lin == q.lin && !memcmp(&s.tn0, &q.tn0, 4) &&
-                            !memcmp(&s.tn1, &q.tn1, 4) && !memcmp(&s.tn2, &q.tn2, 4) &&
-                            (e1 == kInf || (c1 == c3 && q.pc == pack_cell(s.c0, s.c1, s.c2)));
-        if (!same || !same_p) {
+        const float e4 = ex4 ? kInf : tc4;
+        bool same_v = !memcmp(&e1, &e4, 4) && !memcmp(&s.tn0, &x.tn0, 4) && !memcmp(&s.tn1, &x.tn1, 4) &&
+                      !memcmp(&s.tn2, &x.tn2, 4);
+        if (e1 != kInf) {
+            const uint32_t kk = (((x.pc & pk.low2) * pk.kmul) >> pk.kshr) & 63u;
+            const uint32_t kw = (s.c0 & 3u) | (s.c1 & 3u) << 2 | (s.c2 & 3u) << 4;
+            same_v = same_v && c1 == c4 && x.pc == pack_cellv(pk, s.c0, s.c1, s.c2) && kk == kw &&
+                     (!linear || x.pc == s.lin);
+        }
+        if (!same || !same_v) {
             ++g_walk_fails;
             return;
         }

@@ -165,37 +165,95 @@ ZHD void ddaw_from(const Dda& d, const GridK& g, DdaW& w) {
         (D).l1 = (C) ? (A).l1 : (B).l1; (D).l2 = (C) ? (A).l2 : (B).l2;              \
     } while (0)
 
-// The park walk's state with the cell packed into one word (grids of at most
-// 1024 cells per axis): pc = c0 | c1 << 10 | c2 << 20.  A step adds the
-// axis's packed step d_a (+-1 << 10a mod 2^32), the crossing test is one xor
-// and mask, the exit test compares the axis's field with the packed exit
-// cells pe.  Same booleans, same f32 adds, same cells, linear index and
-// T_EXIT as DDAW_STEP (tests/cpp/dda_skip_check.cpp).  A step past the exit
-// (T_EXIT = +inf) may carry into the next field; the walk ends there, and
-// the park kernel's speculative second step only reads a clamped brick.
-struct DdaP {
-    float tn0, tn1, tn2, td0, td1, td2;
-    uint32_t pc, lin, pe;
-    uint32_t d0, d1, d2;      // packed cell step per axis
-    uint32_t s0, l1, l2;      // linear-index step per axis (axis 0: s0)
+// The packed walk state (the park walk and the primary lane walk, grids of
+// at most 1024 cells per axis): the cell in one word of per-grid fields,
+// pc = c0 | c1 << o1 | c2 << o2, field a B_a = max(2, ceil(log2 res_a)) bits
+// wide (o1 = B0, o2 = B0 + B1, B0 + B1 + B2 <= 30).  For res_a = 2^B_a the
+// word IS linearlizeCellIdx (linalg.zig:429-431), and otherwise it indexes a
+// copy of the cells padded to 2^B0 x 2^B1 x 2^B2, so the walk keeps no
+// separate linear index.  A step adds the axis's packed step d_a
+// (+-1 << o_a mod 2^32); the brick-crossing test is one xor and mask; the
+// exit test compares the axis's field with the packed exit cells pe.  Same
+// booleans, same f32 adds, same cells and T_EXIT as DDA_STEP
+// (tests/cpp/dda_skip_check.cpp, step by step on random grids).  A step past
+// the exit (T_EXIT = +inf) may carry into the next field; the walk ends there
+// (the park kernel's speculative second step only reads a clamped brick).
+struct PackK {
+    uint32_t o1, o2;          // bit offsets of fields 1 and 2 (field 0 at bit 0)
+    uint32_t b0, b1, b2;      // field widths
+    uint32_t f0, f1, f2;      // field masks
+    uint32_t low2;            // in-brick bits of every field, 4^3 bricks
+    uint32_t kmul, kshr;      // in-brick cell index: ((pc & low2) * kmul) >> kshr = x | y << 2 | z << 4
 };
-constexpr uint32_t kPackF0 = 0x3FFu, kPackF1 = 0x3FFu << 10, kPackF2 = 0x3FFu << 20;
-constexpr uint32_t kPackLow2 = 3u | (3u << 10) | (3u << 20);   // in-brick bits, 4^3 bricks
-constexpr uint32_t kPackMaxRes = 1024;                         // cells per axis a DdaP holds
-ZHD uint32_t pack_cell(uint32_t c0, uint32_t c1, uint32_t c2) { return c0 | (c1 << 10) | (c2 << 20); }
-ZHD void ddap_from(const Dda& d, const GridK& g, DdaP& w) {
+constexpr uint32_t kPackMaxRes = 1024;                         // cells per axis a packed walk holds
+ZHD uint32_t ceil_log2u(uint32_t x) {
+    uint32_t b = 0;
+    while (b < 32 && (1ull << b) < x) ++b;
+    return b;
+}
+// The layout for given field widths; false if the in-brick index multiplier
+// does not work for it.  The multiplier sums the three fields' low two bits,
+// shifted to x | y << 2 | z << 4: exact when no two of the nine shifted bit
+// pairs overlap (then the sum has no carry); checked here for every in-brick
+// cell, which is exactly the function the kernels compute.
+ZHD bool pack_fields(uint32_t b0, uint32_t b1, uint32_t b2, PackK& k) {
+    if (b0 + b1 + b2 > 30u) return false;
+    k.b0 = b0; k.b1 = b1; k.b2 = b2;
+    k.o1 = b0;
+    k.o2 = b0 + b1;
+    k.f0 = (1u << b0) - 1u;
+    k.f1 = ((1u << b1) - 1u) << k.o1;
+    k.f2 = ((1u << b2) - 1u) << k.o2;
+    k.low2 = 3u | (3u << k.o1) | (3u << k.o2);
+    uint32_t sh = 0;
+    if (k.o1 > 2u + sh) sh = k.o1 - 2u;
+    if (k.o2 > 4u + sh) sh = k.o2 - 4u;
+    k.kshr = sh;
+    k.kmul = (1u << sh) + (1u << (sh + 2u - k.o1)) + (1u << (sh + 4u - k.o2));
+    if (k.kmul >= (1u << 24)) return false;                    // a 24-bit multiply operand
+    for (uint32_t c = 0; c < 64; ++c) {
+        const uint32_t t = (c & 3u) | (((c >> 2) & 3u) << k.o1) | ((c >> 4) << k.o2);
+        if ((((t * k.kmul) >> k.kshr) & 63u) != c) return false;
+    }
+    return true;
+}
+// The layout for a grid; false if it does not pack (an axis above 1024
+// cells).  Fields as narrow as the resolution allows (then the word is the
+// linear index on power-of-two grids), widened where close fields would make
+// the in-brick multiplier's bit pairs overlap (small grids; they then index a
+// padded copy of the cells).
+ZHD bool pack_layout(const uint32_t res[3], PackK& k) {
+    uint32_t b[3];
+    for (int a = 0; a < 3; ++a) {
+        if (res[a] == 0 || res[a] > kPackMaxRes) return false;
+        b[a] = ceil_log2u(res[a]) < 2u ? 2u : ceil_log2u(res[a]);
+    }
+    for (uint32_t extra = 0; extra <= 16; ++extra)            // fewest added bits first
+        for (uint32_t e0 = 0; e0 <= extra; ++e0)
+            if (pack_fields(b[0] + e0, b[1] + (extra - e0), b[2], k)) return true;
+    return false;
+}
+ZHD uint32_t pack_cellv(const PackK& k, uint32_t c0, uint32_t c1, uint32_t c2) {
+    return c0 | (c1 << k.o1) | (c2 << k.o2);
+}
+// whether the packed word equals the linear cell index (no padded copy needed)
+ZHD bool pack_is_linear(const uint32_t res[3], const PackK& k) {
+    return res[0] == (1u << k.b0) && res[1] == (1u << k.b1) && res[2] == (1u << k.b2);
+}
+struct DdaV {
+    float tn0, tn1, tn2, td0, td1, td2;
+    uint32_t pc, pe;
+    uint32_t d0, d1, d2;      // packed cell step per axis
+};
+ZHD void ddav_from(const Dda& d, const GridK& g, const PackK& k, DdaV& w) {
     w.tn0 = d.tn0; w.tn1 = d.tn1; w.tn2 = d.tn2;
     w.td0 = d.td0; w.td1 = d.td1; w.td2 = d.td2;
-    w.pc = pack_cell(d.c0, d.c1, d.c2);
-    w.lin = d.lin;
+    w.pc = pack_cellv(k, d.c0, d.c1, d.c2);
     const bool n0 = d.neg & 1u, n1 = (d.neg >> 1) & 1u, n2 = (d.neg >> 2) & 1u;
-    w.pe = pack_cell(n0 ? 0u : g.rm0, n1 ? 0u : g.rm1, n2 ? 0u : g.rm2);
+    w.pe = pack_cellv(k, n0 ? 0u : g.rm0, n1 ? 0u : g.rm1, n2 ? 0u : g.rm2);
     w.d0 = n0 ? 0xFFFFFFFFu : 1u;
-    w.d1 = n1 ? 0u - (1u << 10) : (1u << 10);
-    w.d2 = n2 ? 0u - (1u << 20) : (1u << 20);
-    w.s0 = w.d0;
-    w.l1 = n1 ? 0u - g.str1 : g.str1;
-    w.l2 = n2 ? 0u - g.str2 : g.str2;
+    w.d1 = n1 ? 0u - (1u << k.o1) : (1u << k.o1);
+    w.d2 = n2 ? 0u - (1u << k.o2) : (1u << k.o2);
 }
 // An opaque copy: keeps the compiler from merging `a0 ? t2 : (a1 ? t2 : u)`
 // into `(a0 || a1) ? t2 : u`, whose or-of-compares it turns into a select of
@@ -207,38 +265,38 @@ ZHD float opaque_f(float x) {
 #endif
     return x;
 }
-// LOWM: the in-brick bits of every field (4^3 bricks: 3 | 3 << 10 | 3 << 20)
-#define DDAP_STEP(S, LOWM, CROSSED, T_EXIT)                                            \
+// One Iterator.next on the packed state.  LOWM: the in-brick bits of every
+// field for the walk's occupancy bricks (CROSSED: the step left its brick).
+// T_EXIT = EXITED ? +inf : TC, so traceRay's break test nearest <= T_EXIT is
+// EXITED || nearest <= TC (nearest is +inf or a hit t, never NaN): one
+// compare and a scalar or, not a select and two compares.
+#define DDAV_STEPX(S, K, LOWM, CROSSED, EXITED, TC)                                   \
     do {                                                                             \
         const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                     \
         const bool b01_ = t0_ < t1_, b02_ = t0_ < t2_, b12_ = t1_ < t2_;             \
         const bool a0_ = b01_ && b02_;                                               \
         const bool a1_ = !b01_ && b12_;                                              \
-        const bool a2_ = !a0_ && !a1_;                                               \
         const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
         const float dt_ = a0_ ? (S).td0 : (a1_ ? (S).td1 : (S).td2);                 \
-        const uint32_t fm_ = a0_ ? kPackF0 : (a1_ ? kPackF1 : kPackF2);              \
+        const uint32_t fm_ = a0_ ? (K).f0 : (a1_ ? (K).f1 : (K).f2);                 \
         const uint32_t pn_ = (S).pc + (a0_ ? (S).d0 : (a1_ ? (S).d1 : (S).d2));      \
-        (S).lin += a0_ ? (S).s0 : (a1_ ? (S).l1 : (S).l2);                           \
         (CROSSED) = (((S).pc ^ pn_) & ~(LOWM)) != 0u;                                \
-        (T_EXIT) = (((S).pc ^ (S).pe) & fm_) == 0u ? kInf : tc_;                     \
+        (EXITED) = (((S).pc ^ (S).pe) & fm_) == 0u;                                  \
+        (TC) = tc_;                                                                  \
         const float un_ = tc_ + dt_;                                                 \
         (S).tn0 = a0_ ? un_ : t0_;                                                   \
         (S).tn1 = a1_ ? un_ : t1_;                                                   \
-        (S).tn2 = a0_ ? t2_ : (a1_ ? opaque_f(t2_) : un_);    /* a2_: neither */     \
-        (void)a2_;                                                                   \
+        (S).tn2 = a0_ ? t2_ : (a1_ ? opaque_f(t2_) : un_);    /* a2: neither */       \
         (S).pc = pn_;                                                                \
     } while (0)
-#define DDAP_SEL(D, C, A, B)                                                          \
+#define DDAV_SEL(D, C, A, B)                                                          \
     do {                                                                             \
         (D).tn0 = (C) ? (A).tn0 : (B).tn0; (D).tn1 = (C) ? (A).tn1 : (B).tn1;        \
         (D).tn2 = (C) ? (A).tn2 : (B).tn2; (D).td0 = (C) ? (A).td0 : (B).td0;        \
         (D).td1 = (C) ? (A).td1 : (B).td1; (D).td2 = (C) ? (A).td2 : (B).td2;        \
-        (D).pc = (C) ? (A).pc : (B).pc; (D).lin = (C) ? (A).lin : (B).lin;           \
-        (D).pe = (C) ? (A).pe : (B).pe; (D).d0 = (C) ? (A).d0 : (B).d0;              \
-        (D).d1 = (C) ? (A).d1 : (B).d1; (D).d2 = (C) ? (A).d2 : (B).d2;              \
-        (D).s0 = (C) ? (A).s0 : (B).s0; (D).l1 = (C) ? (A).l1 : (B).l1;              \
-        (D).l2 = (C) ? (A).l2 : (B).l2;                                              \
+        (D).pc = (C) ? (A).pc : (B).pc; (D).pe = (C) ? (A).pe : (B).pe;              \
+        (D).d0 = (C) ? (A).d0 : (B).d0; (D).d1 = (C) ? (A).d1 : (B).d1;              \
+        (D).d2 = (C) ? (A).d2 : (B).d2;                                              \
     } while (0)
 
 // Empty-brick skip, 4^3 bricks (occ_shift 2): the state Iterator.next would

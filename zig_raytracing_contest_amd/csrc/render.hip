@@ -63,18 +63,38 @@ constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue e
 // cfg2 +0.9%, cfg5 +0.2%; 4: +0.6 / +0.5 / 0%)
 constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 
+// Triangle positions per ref (bakeInto's Pos: v0, e1 = v1 - v0, e2 = v2 - v0).
+// ZRT_TRI36: 9 floats (36 B) per ref, read as two dword-aligned 16-byte loads
+// and one dword; otherwise 3 float4 (48 B, w unused).  A cell's refs are
+// contiguous, so 36 B touches 25% fewer cache lines per cell.
+#ifndef ZRT_TRI36
+#define ZRT_TRI36 0
+#endif
+constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
+struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+
 struct TraceParams {
     float bmin[3], bmax[3];
     uint32_t res[3];
     float cs[3];
     const uint2* cells;
-    const float4* tri_pos;    // 3 per ref: v0, e1, e2 (w unused)
+    const float* tri_pos;     // kTriFloats per ref (see kTriFloats)
     const float4* tri_data;   // 4 per ref: n0 n1 n2 uv0 uv1 uv2 mat
     const DevMat* mats;
+    uint32_t nmat;
     const float* texels;
     const double* zig;        // zx[257], zf[257]
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
+    // packed walks (DdaV): the layout, the cells indexed by the packed word
+    // (the cells themselves for power-of-two grids, else a padded copy), the
+    // coarse-brick fields of the packed word (offset, width per axis) and
+    // their in-brick bits; the 4^3-brick fields for OccX
+    PackK pk;
+    const uint2* cells_v;
+    uint32_t occ_o1, occ_o2, occ_w0, occ_w1, occ_w2, occ_lowm;
+    uint32_t ox1, ox2, ow0, ow1, ow2;
     float org[3], llc[3], right[3], up[3];
     uint32_t w;
     const uint32_t* pixlist;
@@ -87,6 +107,20 @@ struct TraceParams {
     uint32_t* counter;
     unsigned long long* stats;   // segments, cells, tests, hits, diagnostics
 };
+
+// Ref j's v0, e1, e2.
+__device__ __forceinline__ void load_tri(const TraceParams& p, uint32_t j, v3& v0, v3& e1, v3& e2) {
+    const float* q = p.tri_pos + (uint64_t)kTriFloats * j;
+    if constexpr (ZRT_TRI36) {
+        const f4u a = *reinterpret_cast<const f4u*>(q), b = *reinterpret_cast<const f4u*>(q + 4);
+        const float c = q[8];
+        v0 = mk(a.x, a.y, a.z); e1 = mk(a.w, b.x, b.y); e2 = mk(b.z, b.w, c);
+    } else {
+        const float4 a = *reinterpret_cast<const float4*>(q), b = *reinterpret_cast<const float4*>(q + 4),
+                     c = *reinterpret_cast<const float4*>(q + 8);
+        v0 = mk(a.x, a.y, a.z); e1 = mk(b.x, b.y, b.z); e2 = mk(c.x, c.y, c.z);
+    }
+}
 
 // Per-bounce (emissive, albedo) pairs of one path (counting megakernel only).
 // The fold reads them back to front: e0 + a0*(e1 + a1*(...)) is
@@ -120,12 +154,12 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
-// brick_occupied for a packed cell (DdaP, 10 bits per axis)
-__device__ __forceinline__ bool brick_occupied_p(const TraceParams& p, const uint32_t* occ, uint32_t pc) {
-    const uint32_t s = p.occ_shift;
-    const uint32_t m = 0x3FFu >> s;
-    const uint32_t b = __umul24((pc >> (20u + s)) & m, p.occ_nb01) + __umul24((pc >> (10u + s)) & m, p.occ_nb0) +
-                       ((pc >> s) & m);
+// brick_occupied for a packed cell (DdaV): the brick coordinates are bit
+// fields of the word (width 0 when a brick spans the whole axis)
+__device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uint32_t* occ, uint32_t pc) {
+    const uint32_t b = __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o2, p.occ_w2), p.occ_nb01) +
+                       __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
+                       __builtin_amdgcn_ubfe(pc, p.occ_shift, p.occ_w0);
     return (occ[b >> 5] >> (b & 31u)) & 1u;
 }
 
@@ -153,21 +187,15 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
                                           uint32_t& n_tests, uint64_t* wstat) {
     for (uint32_t i = b; i < e; i += TB) {
         if (STATS && first_active_lane()) ++wstat[1];   // wave trips of this loop
-        float4 A[TB], B[TB], Cc[TB];
+        v3 A[TB], B[TB], Cc[TB];
 #pragma unroll
-        for (int k = 0; k < TB; ++k) {
-            const uint32_t j = min(i + (uint32_t)k, e - 1u);
-            A[k] = p.tri_pos[3 * j + 0];
-            B[k] = p.tri_pos[3 * j + 1];
-            Cc[k] = p.tri_pos[3 * j + 2];
-        }
+        for (int k = 0; k < TB; ++k) load_tri(p, min(i + (uint32_t)k, e - 1u), A[k], B[k], Cc[k]);
 #pragma unroll
         for (int k = 0; k < TB; ++k) {
             if (i + (uint32_t)k < e) {
                 if (STATS) ++n_tests;
                 float t, u, v;
-                if (tri_ray(mk(A[k].x, A[k].y, A[k].z), mk(B[k].x, B[k].y, B[k].z),
-                            mk(Cc[k].x, Cc[k].y, Cc[k].z), o, d, &t, &u, &v)) {
+                if (tri_ray(A[k], B[k], Cc[k], o, d, &t, &u, &v)) {
                     if (nearest > t && t > 0.0f) { nearest = t; hu = u; hv = v; hidx = i + k; }
                 }
             }
@@ -183,8 +211,9 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // [6] cell loads, [7] non-empty cells, [8] wave trips of the cell loop,
 // [9] wave trips of the triangle-batch loop, [10] cell trips with any test,
 // [4] 64-wide rounds if each trip's tests were shared evenly.
-// PACKED: the walk state with the cell packed into one word (DdaP, grids of
-// at most 1024 cells per axis; same cells, same order, same t_exit).
+// PACKED: the walk state with the cell packed into one word (DdaV, grids of
+// at most 1024 cells per axis; same cells, same order, same t_exit), which
+// also indexes the cells (cells_v).
 template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
@@ -196,20 +225,19 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
     const GridK gk = grid_consts(p);
     if constexpr (PACKED) {
         static_assert(!STATS, "the counting build walks unpacked");
-        DdaP s;
-        ddap_from(s0, gk, s);
-        const uint32_t lowm = ((1u << sh) - 1u) * (1u | (1u << 10) | (1u << 20));
-        bool occupied = brick_occupied_p(p, occ, s.pc);
+        DdaV s;
+        ddav_from(s0, gk, p.pk, s);
+        bool occupied = brick_occupied_v(p, occ, s.pc);
         for (;;) {
             if (occupied) {
-                const uint2 cell = p.cells[s.lin];
+                const uint2 cell = p.cells_v[s.pc];
                 test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
             }
-            bool crossed;
-            float t_exit;
-            DDAP_STEP(s, lowm, crossed, t_exit);
-            if (nearest <= t_exit) break;                  // stage3.zig:179-182
-            if (crossed) occupied = brick_occupied_p(p, occ, s.pc);
+            bool crossed, exited;
+            float tc;
+            DDAV_STEPX(s, p.pk, p.occ_lowm, crossed, exited, tc);
+            if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
+            if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
         return nearest;
     }
@@ -457,10 +485,11 @@ __device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
 // bounce planes on a scatter, pass-through otherwise.  Returns true when the
 // path continues (o, d, depth, slot, rng, mask updated); false with L set
 // when it terminates.
+// `mats`: the material descriptors (p.mats, or the shade kernel's LDS copy).
 __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* zx, const double* zf,
-                                              uint32_t item, float t, float hu, float hv, uint32_t hidx,
-                                              v3& o, v3& d, uint32_t& depth, uint32_t& slot, Rng& rng,
-                                              uint32_t& mask, v3& L) {
+                                              const DevMat* mats, uint32_t item, float t, float hu, float hv,
+                                              uint32_t hidx, v3& o, v3& d, uint32_t& depth, uint32_t& slot,
+                                              Rng& rng, uint32_t& mask, v3& L) {
     const TraceParams& p = w.t;
     if (t == kInf) { L = env_color(d); return false; }     // stage3.zig:195-197
     const float4* tdp = p.tri_data + 4ull * hidx;          // stage3.zig:199-206
@@ -468,7 +497,7 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
     const float w0 = 1.0f - hu - hv;
     const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
     const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
-    const DevMat& m = p.mats[__float_as_uint(d3.w)];
+    const DevMat& m = mats[__float_as_uint(d3.w)];
     const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
     const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
     const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
@@ -632,7 +661,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             v3 L = mk(0, 0, 0);
             if (depth != 0) {
                 ++n_seg;
-                cont = shade_segment(w, zx, zf, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
+                cont = shade_segment(w, zx, zf, p.mats, item, t, hu, hv, hidx, o, d, depth, slot, rng, mask, L);
             }
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
@@ -673,19 +702,24 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 // Per lane the cells, the tests, their order semantics and the break test
 // after every cell (stage3.zig:179-182) are the reference's: same hit.
 //
-// OccX (4^3-cell bricks): one bit per brick, the u16 number of occupied
-// bricks before each 32-brick word, one 64-bit cell mask per occupied brick
-// (+ one zero mask).
+// OccX (4^3-cell bricks): one bit per brick, 1 + the u16 number of
+// occupied bricks before each 32-brick word, the zero mask, then one 64-bit
+// cell mask per occupied brick.
 // In LDS each 32-brick word sits beside its prefix as one 8-byte entry, so a
-// lookup is two dependent LDS reads: (bits, prefix), then the mask.
+// lookup is two dependent LDS reads: (bits, prefix), then the mask.  The
+// mask index is (1 + prefix + occupied bricks below b in the word) x (b's
+// bit): an empty brick reads the zero mask at index 0, so nothing is
+// selected after the load (5 VALU from the entry to the mask address,
+// against 11 with the loaded mask zeroed by selects; the bit-field
+// extracts use the hardware's 5-bit offset/width, so b needs no & 31).
 struct OccX {
-    const uint2* ent;                    // (brick bits, occupied bricks before the word)
-    const unsigned long long* masks;
+    const uint2* ent;                    // (brick bits, 1 + occupied bricks before the word)
+    const unsigned long long* masks;     // [0]: zero mask
 };
 __device__ __forceinline__ unsigned long long occx_mask_at(const OccX& L, uint2 e, uint32_t b) {
-    const uint32_t below = (uint32_t)__popc(e.x & ((1u << (b & 31u)) - 1u));
-    const unsigned long long m = L.masks[e.y + below];  // <= occupied count: the zero mask at worst
-    return ((e.x >> (b & 31u)) & 1u) ? m : 0ull;
+    const uint32_t low = __builtin_amdgcn_ubfe(e.x, 0u, b);        // bits of the bricks below b
+    const uint32_t bit = __builtin_amdgcn_ubfe(e.x, b, 1u);
+    return L.masks[__umul24((uint32_t)__popc(low) + e.y, bit)];
 }
 __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
     return occx_mask_at(L, L.ent[b >> 5], b);
@@ -696,30 +730,23 @@ __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t 
 __device__ __forceinline__ unsigned long long occx_mask_clamped(const OccX& L, uint32_t b, uint32_t nbw) {
     return occx_mask_at(L, L.ent[min(b >> 5, nbw - 1u)], b);
 }
-// brick index: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate),
-// exact because a grid of more than 2^24 bricks is rejected at context
-// creation (their bits would not fit the LDS)
-template <class D>
-__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const D& s) {
-    return __umul24(s.c2 >> 2, w.occx_nb01) + __umul24(s.c1 >> 2, w.occx_nb0) + (s.c0 >> 2);
+// The 4^3 brick of a packed cell (DdaV): its coordinates are the fields'
+// bits above their low two.  24-bit multiplies (full rate; v_mul_lo_u32 is
+// quarter rate), exact because OccX serves only grids of at most 2^24
+// bricks (occx_usable).
+__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaV& s) {
+    const TraceParams& p = w.t;
+    return __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox2, p.ow2), w.occx_nb01) +
+           __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox1, p.ow1), w.occx_nb0) + __builtin_amdgcn_ubfe(s.pc, 2u, p.ow0);
 }
-// the same two from a packed cell (DdaP, fields of 10 bits)
-__device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaP& s) {
-    return __umul24((s.pc >> 22) & 0xFFu, w.occx_nb01) + __umul24((s.pc >> 12) & 0xFFu, w.occx_nb0) +
-           ((s.pc >> 2) & 0xFFu);
-}
-__device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaP& s) {
-    const uint32_t half = (s.pc & (2u << 20)) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
-    const uint32_t k = ((s.pc >> 16) & 0x10u) | ((s.pc >> 8) & 0xCu) | (s.pc & 3u);
-    return (half >> k) & 1u;
-}
-// bit of cell (c0, c1, c2) in its brick's 64-bit mask, tested on the 32-bit
-// half that holds it (bit 5 of the index is bit 1 of c2)
-template <class D>
-__device__ __forceinline__ bool occx_cell(unsigned long long bm, const D& s) {
-    const uint32_t half = (s.c2 & 2u) ? (uint32_t)(bm >> 32) : (uint32_t)bm;
-    const uint32_t k = ((s.c2 & 1u) << 4) | ((s.c1 & 3u) << 2) | (s.c0 & 3u);
-    return (half >> k) & 1u;
+// The in-brick cell index k = x | y << 2 | z << 4 of a packed cell: one
+// 24-bit multiply of the fields' low two bits sums them, shifted into place
+// (pack_layout picks the multiplier and checks every in-brick cell), and the
+// 64-bit shift reads only k[5:0].  (6 VALU; 9 with the fields moved by shifts
+// and masks.)
+__device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
+    const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
+    return (uint32_t)(bm >> (i & 63u)) & 1u;
 }
 
 // A parked lane's cell range [begin, end) is loaded by LDS-DMA into its
@@ -748,8 +775,8 @@ constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 // register: the clobber is ignored), so nothing else in the park kernel may
 // rely on it: tests/test_codegen.py checks that every M0 access in its code
 // object is this sequence.
-__device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t lin, uint32_t* rng) {
-    const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells) + 2ull * lin;
+__device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t pc, uint32_t* rng) {
+    const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells_v) + 2ull * pc;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rng);
     // (an instruction offset would move the LDS destination too: the end
     // word gets its own address)
@@ -837,17 +864,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t cb = 0, ce = 0, cgrp = 0;     // the wave's current chunk of queue entries
     // the segment: ray, DDA state, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-#ifdef ZRT_UNPACKED_WALK
-    DdaW s;
-#define PARK_FROM ddaw_from
-#define PARK_STEP(S, CR, TE) DDAW_STEP(S, 2u, CR, TE)
-#define PARK_SEL DDAW_SEL
-#else
-    DdaP s;                                // grids of <= 1024 cells per axis (zrt_context_render)
-#define PARK_FROM ddap_from
-#define PARK_STEP(S, CR, TE) DDAP_STEP(S, kPackLow2, CR, TE)
-#define PARK_SEL DDAP_SEL
-#endif
+    DdaV s;                                // grids of <= 1024 cells per axis (zrt_context_render)
+    const PackK pk = p.pk;
+#define PARK_STEP(S, CR, EX, TC) DDAV_STEPX(S, pk, pk.low2, CR, EX, TC)
     memset(&s, 0, sizeof s);
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
@@ -903,9 +922,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
                             Dda s0;
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
-                                PARK_FROM(s0, gk, s);
-                                if (occx_cell(occx_mask(L, occx_brick(w, s)), s)) {
-                                    park_load_range(p, s.lin, rng_slot);
+                                ddav_from(s0, gk, pk, s);
+                                if (occx_cell(occx_mask(L, occx_brick(w, s)), s, pk)) {
+                                    park_load_range(p, s.pc, rng_slot);
                                     st = kPark;
                                 } else {
                                     st = kWalk;
@@ -939,11 +958,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // speculative and dropped when the first cell parks or ends
                 // the segment (its lookup then reads a clamped brick)
                 auto s1 = s;
-                bool cr1, cr2;
+                bool cr1, cr2, ex1, ex2;
                 float te1, te2;
-                PARK_STEP(s1, cr1, te1);
+                PARK_STEP(s1, cr1, ex1, te1);
                 auto s2 = s1;
-                PARK_STEP(s2, cr2, te2);
+                PARK_STEP(s2, cr2, ex2, te2);
                 unsigned long long q1 = occx_mask_clamped(L, occx_brick(w, s1), w.occx_nbw);
                 unsigned long long q2 = occx_mask_clamped(L, occx_brick(w, s2), w.occx_nbw);
                 // both lookups complete here, ahead of the selects below
@@ -965,14 +984,15 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // segment (stage3.zig:179-182) or holds triangles; selects,
                 // not branches: the branchy form made the compiler copy the
                 // whole state through every join (up to 232 VALU per trip)
-                const bool d1 = nearest <= te1, d2 = nearest <= te2;
-                const bool o1 = occx_cell(m1, s1), o2 = occx_cell(m2, s2);
+                // traceRay's break test nearest <= T_EXIT, T_EXIT = +inf at the exit
+                const bool d1 = ex1 || nearest <= te1, d2 = ex2 || nearest <= te2;
+                const bool o1 = occx_cell(m1, s1, pk), o2 = occx_cell(m2, s2, pk);
                 const bool at1 = d1 || o1;
-                const bool pk = at1 ? !d1 : (!d2 && o2);
+                const bool pkd = at1 ? !d1 : (!d2 && o2);
                 if (at1 ? d1 : d2) st = kDone;
-                PARK_SEL(s, at1, s1, s2);
-                if (pk) {                                          // one issue point per trip
-                    park_load_range(p, s.lin, rng_slot);
+                DDAV_SEL(s, at1, s1, s2);
+                if (pkd) {                                         // one issue point per trip
+                    park_load_range(p, s.pc, rng_slot);
                     st = kPark;
                 }
             }
@@ -1010,9 +1030,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 bool cand = false;
                 float t = 0.0f, u = 0.0f, v = 0.0f;
                 if (g < tot) {
-                    const float4 A = p.tri_pos[3ull * j], B = p.tri_pos[3ull * j + 1], C = p.tri_pos[3ull * j + 2];
-                    cand = tri_ray_flat(mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z),
-                                        mk(ro.x, ro.y, ro.z), mk(rd.x, rd.y, rd.z), &t, &u, &v) &&
+                    v3 A, B, C;
+                    load_tri(p, j, A, B, C);
+                    cand = tri_ray_flat(A, B, C, mk(ro.x, ro.y, ro.z), mk(rd.x, rd.y, rd.z), &t, &u, &v) &&
                            ro.w > t && t > 0.0f;                   // stage3.zig:172
                 }
                 const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
@@ -1036,9 +1056,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         PARK_STAMP(2);
     }
     __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
-#undef PARK_FROM
 #undef PARK_STEP
-#undef PARK_SEL
 #ifdef ZRT_SWEEP
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
@@ -1052,7 +1070,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 // One path of the shading half, its state decoded and its hit record h
 // loaded: shades, writes the terminal radiance of an ending path and appends
 // a continuing one (the whole wave calls it).
-__device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, const double* zf, bool valid,
+__device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, const double* zf,
+                                           const DevMat* mats, bool valid,
                                            uint32_t item, v3 o, v3 d, uint32_t depth, uint32_t slot, Rng rng,
                                            uint32_t mask, float4 h, uint64_t below, uint32_t grp,
                                            uint32_t& n_seg) {
@@ -1060,29 +1079,40 @@ __device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, 
     if (valid) {
         v3 L = mk(0, 0, 0);
         ++n_seg;                               // queued / primary paths have depth >= 1
-        cont = shade_segment(w, zx, zf, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot, rng,
-                             mask, L);
+        cont = shade_segment(w, zx, zf, mats, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot,
+                             rng, mask, L);
         if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
     }
     wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
 }
 
 // One queue entry: its path record (a, b, c) and hit record h already loaded.
-__device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf, bool valid,
+__device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf,
+                                            const DevMat* mats, bool valid,
                                             float4 a, float4 b, float4 c, float4 h, uint64_t below,
                                             uint32_t grp, uint32_t& n_seg) {
     Rng rng;
     rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
-    shade_path(w, zx, zf, valid, __float_as_uint(a.w), mk(a.x, a.y, a.z), mk(b.x, b.y, b.z),
+    shade_path(w, zx, zf, mats, valid, __float_as_uint(a.w), mk(a.x, a.y, a.z), mk(b.x, b.y, b.z),
                __float_as_uint(b.w) & 0xFFFFu, __float_as_uint(b.w) >> 16, rng, __float_as_uint(c.z), h, below,
                grp, n_seg);
 }
 
+// LMATS: the material descriptors (at most kLdsMats) copied to LDS, so the
+// dependent chain hit -> triangle data -> material -> texels takes its
+// material hop from LDS instead of L2.
+constexpr uint32_t kLdsMats = 64;
+template <bool LMATS>
 __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
+    __shared__ DevMat s_mats[LMATS ? kLdsMats : 1];
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
+    if (LMATS)
+        for (uint32_t i = threadIdx.x; i < p.nmat * (uint32_t)(sizeof(DevMat) / 4); i += blockDim.x)
+            reinterpret_cast<uint32_t*>(s_mats)[i] = reinterpret_cast<const uint32_t*>(p.mats)[i];
     __syncthreads();
+    const DevMat* const mats = LMATS ? s_mats : p.mats;
     const double* zx = s_zig;
     const double* zf = s_zig + 257;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1111,7 +1141,7 @@ __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w)
         }
 #pragma unroll
         for (int e = 0; e < kShadeEntries; ++e)
-            shade_entry(w, zx, zf, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg);
+            shade_entry(w, zx, zf, mats, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -1266,7 +1296,11 @@ struct zrt_context {
     zrt_grid grid{};
     uint32_t ncells = 0, nrefs = 0, nmat = 0;
     uint2* d_cells = nullptr;
-    float4* d_pos = nullptr;
+    // packed walks (DdaV): the layout and the cells indexed by the packed word
+    PackK pk{};
+    bool packed = false;
+    uint2* d_cells_v = nullptr;        // == d_cells for power-of-two grids, else a padded copy (owned)
+    float* d_pos = nullptr;
     float4* d_data = nullptr;
     DevMat* d_mats = nullptr;
     float* d_texels = nullptr;
@@ -1364,7 +1398,7 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelE,wf_shade_kernelE,wf_kernelILi" ZRT_STR(
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelE,wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(
         ZRT_WF_MINW) "ELb0ELb1EE";
 #undef ZRT_STR
 #undef ZRT_STR2
@@ -1388,6 +1422,7 @@ extern "C" int zrt_device_warmup(int device) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
+    if (c->d_cells_v && c->d_cells_v != c->d_cells) (void)hipFree(c->d_cells_v);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
@@ -1435,9 +1470,9 @@ __global__ __launch_bounds__(kBlock) void occx_mask_kernel(const uint2* __restri
     if (b < nb && (lane == 0 || lane == 32)) bits[b >> 5] = (uint32_t)(bal >> lane);
 }
 
-// Pass 2 (one block): u16 prefix of occupied bricks per 32-brick word, the
-// occupied masks compacted in brick order, then the zero mask; out[0] = the
-// number of occupied bricks.
+// Pass 2 (one block): 1 + the u16 prefix of occupied bricks per 32-brick
+// word, the zero mask, then the occupied masks compacted in brick order;
+// out[0] = the number of occupied bricks.
 __global__ __launch_bounds__(1024) void occx_pack_kernel(const uint32_t* __restrict__ bits, uint32_t nbw,
                                                          const unsigned long long* __restrict__ masks,
                                                          uint16_t* __restrict__ prefix,
@@ -1458,16 +1493,25 @@ __global__ __launch_bounds__(1024) void occx_pack_kernel(const uint32_t* __restr
     }
     uint32_t run = part[threadIdx.x] - sum;
     for (uint32_t wd = w0; wd < w1; ++wd) {
-        prefix[wd] = (uint16_t)min(run, 0xFFFFu);
-        for (uint32_t wb = bits[wd]; wb; wb &= wb - 1u) packed[run++] = masks[32u * wd + (uint32_t)__builtin_ctz(wb)];
+        prefix[wd] = (uint16_t)min(run + 1u, 0xFFFFu);
+        for (uint32_t wb = bits[wd]; wb; wb &= wb - 1u)
+            packed[1u + run++] = masks[32u * wd + (uint32_t)__builtin_ctz(wb)];
     }
-    if (threadIdx.x == 1023) {
-        packed[run] = 0ull;
-        out[0] = run;
-    }
+    if (threadIdx.x == 0) packed[0] = 0ull;
+    if (threadIdx.x == 1023) out[0] = run;
 }
 
 }  // namespace
+
+// 3 float4 per ref (the device bake's layout) -> kTriFloats = 9 floats per ref.
+__global__ __launch_bounds__(kBlock) void tri_repack_kernel(const float4* __restrict__ in, uint32_t refs,
+                                                           float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= refs) return;
+    const float4 a = in[3ull * i], b = in[3ull * i + 1], c = in[3ull * i + 2];
+    float* o = out + 9ull * i;
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = b.x; o[4] = b.y; o[5] = b.z; o[6] = c.x; o[7] = c.y; o[8] = c.z;
+}
 
 static int context_base(zrt_context* c) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1482,7 +1526,47 @@ static int context_base(zrt_context* c) {
 static int context_materials(zrt_context* c, const zrt_scene* s);
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells);
 
+// The cells at their packed-word index (x | y << o1 | z << o2) in a grid
+// padded to powers of two per axis; the padding stays {0, 0} (empty).
+__global__ __launch_bounds__(kBlock) void cells_pad_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                           uint32_t ncells, uint32_t o1, uint32_t o2,
+                                                           uint2* __restrict__ out) {
+    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / r0 / r1;
+        out[x | (y << o1) | (z << o2)] = cells[ci];
+    }
+}
+
+// The packed walks' layout (DdaV) and, for a grid whose resolution is not a
+// power of two per axis, the padded copy of the cells it indexes (none beyond
+// 16 GiB, or beyond 256 MiB and 16x the cells -- flat grids whose narrow
+// axis pack_layout widened: such a grid walks unpacked).
+constexpr uint64_t kPadCellsMax = 16ull << 30;
+static int context_packed(zrt_context* c) {
+    const uint32_t* r = c->grid.resolution;
+    c->packed = pack_layout(r, c->pk);
+    if (!c->packed) return ZRT_OK;
+    if (pack_is_linear(r, c->pk)) {
+        c->d_cells_v = c->d_cells;
+        return ZRT_OK;
+    }
+    const uint64_t n = 1ull << (c->pk.b0 + c->pk.b1 + c->pk.b2);
+    if (8 * n > kPadCellsMax || (n > 16ull * c->ncells && 8 * n > (256ull << 20))) {
+        c->packed = false;
+        return ZRT_OK;
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_cells_v, 8 * n));
+    HIP_TRY(hipMemsetAsync(c->d_cells_v, 0, 8 * n, c->stream));
+    hipLaunchKernelGGL(cells_pad_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells,
+                       c->pk.o1, c->pk.o2, c->d_cells_v);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ZRT_OK;
+}
+
 static int context_counters(zrt_context* c) {
+    int rc = context_packed(c);
+    if (rc != ZRT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
     return ZRT_OK;
@@ -1498,19 +1582,23 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMalloc((void**)&c->d_cells, 8ull * c->ncells));
     HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
-    std::vector<float4> pos(3 * nr), dat(4 * nr);
+    std::vector<float> pos(kTriFloats * nr, 0.0f);
+    std::vector<float4> dat(4 * nr);
     for (uint32_t i = 0; i < c->nrefs; ++i) {
         const float* q = s->triangles_pos + 9ull * i;
-        pos[3 * i + 0] = make_float4(q[0], q[1], q[2], 0.0f);
-        pos[3 * i + 1] = make_float4(q[3], q[4], q[5], 0.0f);
-        pos[3 * i + 2] = make_float4(q[6], q[7], q[8], 0.0f);
+        float* o = pos.data() + (size_t)kTriFloats * i;
+        if (kTriFloats == 9) {
+            memcpy(o, q, 36);
+        } else {
+            memcpy(o, q, 12); memcpy(o + 4, q + 3, 12); memcpy(o + 8, q + 6, 12);
+        }
         float tmp[16];
         memcpy(tmp, s->triangles_data + 15ull * i, 15 * sizeof(float));
         memcpy(&tmp[15], &s->triangles_material[i], 4);
         memcpy(&dat[4 * i], tmp, 64);
     }
-    HIP_TRY(hipMalloc((void**)&c->d_pos, pos.size() * sizeof(float4)));
-    HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&c->d_pos, pos.size() * sizeof(float)));
+    HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
     HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
     if ((rc = context_materials(c, s)) != ZRT_OK) return rc;
@@ -1545,7 +1633,7 @@ static int context_materials(zrt_context* c, const zrt_scene* s) {
 }
 
 // OccX blob layout for nb bricks (nbw 32-brick words) and `occupied` masks:
-// bits | u16 prefix per word | (8-byte aligned) masks + the zero mask.
+// bits | u16 (1 + prefix) per word | (8-byte aligned) the zero mask + masks.
 static void occx_layout(uint64_t nbw, uint64_t occupied, uint64_t* moff, uint64_t* words) {
     const uint64_t pw = (nbw + 1) / 2;                   // prefix words
     *moff = (nbw + pw + 1) & ~1ull;
@@ -1634,11 +1722,11 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         std::vector<unsigned long long> masks;
         uint64_t run = 0;
         for (uint64_t wd = 0; wd < nbw; ++wd) {
-            prefix[wd] = (uint16_t)std::min<uint64_t>(run, 0xFFFF);
+            prefix[wd] = (uint16_t)std::min<uint64_t>(run + 1, 0xFFFF);
             for (uint64_t b = wd * 32; b < std::min<uint64_t>(nb, wd * 32 + 32); ++b)
                 if (mask[b]) { bits[wd] |= 1u << (b & 31); masks.push_back(mask[b]); ++run; }
         }
-        masks.push_back(0ull);
+        masks.insert(masks.begin(), 0ull);
         uint64_t moff, words;
         occx_layout(nbw, run, &moff, &words);
         c->occx_ok = occx_usable(nb, run, occx_lds_words(nbw, moff, words) * 4, kOccxBudget);
@@ -1778,7 +1866,18 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
             c->ncells = resolution[0] * resolution[1] * resolution[2];
             c->nrefs = dg.refs;
             c->d_cells = dg.cells;
-            c->d_pos = dg.pos;
+            if (kTriFloats == 12) {
+                c->d_pos = reinterpret_cast<float*>(dg.pos);
+            } else {   // the device bake writes 3 float4 per ref: repack to 9 floats
+                HIP_TRY(hipMalloc((void**)&c->d_pos, 36ull * std::max<uint32_t>(dg.refs, 1)));
+                if (dg.refs) {
+                    hipLaunchKernelGGL(tri_repack_kernel, dim3((dg.refs + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                                       c->stream, (const float4*)dg.pos, dg.refs, c->d_pos);
+                    HIP_TRY(hipGetLastError());
+                    HIP_TRY(hipStreamSynchronize(c->stream));
+                }
+                (void)hipFree(dg.pos);
+            }
             c->d_data = dg.data;
             if ((rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
         }
@@ -1994,18 +2093,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // path, and the fallback).
     // (the park walk packs a cell into one word: at most 1024 cells per axis)
     const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK) &&
-                           c->grid.resolution[0] <= kPackMaxRes && c->grid.resolution[1] <= kPackMaxRes &&
-                           c->grid.resolution[2] <= kPackMaxRes;
+                           c->packed;
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
-    const bool packed = c->grid.resolution[0] <= kPackMaxRes && c->grid.resolution[1] <= kPackMaxRes &&
-                        c->grid.resolution[2] <= kPackMaxRes;
+    const bool packed = c->packed;
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
-    const WfFn s_next = (WfFn)wf_shade_kernel;
+    const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
         if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
 
@@ -2084,9 +2181,27 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         tp.up[i] = cam->up[i];
     }
     tp.cells = c->d_cells;
+    tp.pk = c->pk;
+    tp.cells_v = c->d_cells_v;
+    {
+        const uint32_t sh = c->occ_shift, b[3] = {c->pk.b0, c->pk.b1, c->pk.b2};
+        auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
+        tp.occ_o1 = c->pk.o1 + sh;
+        tp.occ_o2 = c->pk.o2 + sh;
+        tp.occ_w0 = b[0] > sh ? b[0] - sh : 0u;
+        tp.occ_w1 = b[1] > sh ? b[1] - sh : 0u;
+        tp.occ_w2 = b[2] > sh ? b[2] - sh : 0u;
+        tp.occ_lowm = lowbits(0) | (lowbits(1) << c->pk.o1) | (lowbits(2) << c->pk.o2);
+        tp.ox1 = c->pk.o1 + 2u;
+        tp.ox2 = c->pk.o2 + 2u;
+        tp.ow0 = b[0] - 2u;
+        tp.ow1 = b[1] - 2u;
+        tp.ow2 = b[2] - 2u;
+    }
     tp.tri_pos = c->d_pos;
     tp.tri_data = c->d_data;
     tp.mats = c->d_mats;
+    tp.nmat = c->nmat;
     tp.texels = c->d_texels;
     tp.zig = c->d_zig;
     tp.occ = c->d_occ;
