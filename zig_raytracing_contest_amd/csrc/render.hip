@@ -2152,6 +2152,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, f, threads, lds));
+        if (getenv("ZRT_WF_DEBUG"))
+            fprintf(stderr, "{\"zrt_grid\": {\"threads\": %d, \"lds\": %zu, \"blocks_per_cu\": %d}}\n", threads, lds, bpc);
         bpc = std::max(1, std::min(bpc, 2048 / threads));
         *blocks = (uint32_t)(c->num_cus * bpc);
         return ZRT_OK;
