@@ -135,5 +135,5 @@ def test_park_walk_trip_is_not_a_register_shuffle(code):
     assert valu <= 170 and movs <= 40, (valu, movs)
 
 
-def ins_after(ins, e, n=12):
+def ins_after(ins, e, n=40):
     return [t.strip() for _, t in ins[e + 1:e + 1 + n]]

@@ -54,3 +54,35 @@ def test_wave_shared_tests_match_sequential(emul, name, res):
     hits = int(np.isfinite(out_s[:, 0]).sum())
     assert hits > n // 20
     assert bad == 0
+
+
+@pytest.mark.parametrize("name,res", [("cornell", (32, 32, 32)), ("contest", (128, 128, 128)),
+                                      ("sponza", (128, 128, 128)), ("contest", (37, 64, 101))])
+def test_entry_face_skip_is_exact(emul, name, res):
+    """The park kernel's entry-face skip (render.hip cell32_kernel): a ref
+    whose (v0, e1, e2) bits equal a ref of the cell the ray just left is not
+    tested again.  Sequential traceRay with and without the skip, random rays
+    from inside and outside the grid: bit-identical nearest t, u, v and ref;
+    and the skip removes a real share of the tests."""
+    soup = scenes.get_scene(name)
+    geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, resolution=res)
+    g = geo.scene.grid
+    bmin = np.array(g.bbox_min, np.float32)
+    bmax = np.array(g.bbox_max, np.float32)
+    r = np.array(g.resolution, np.uint32)
+    cs = np.array(g.cell_size, np.float32)
+    cells = np.ascontiguousarray(geo.cells().reshape(-1), np.uint32)
+    pos = np.ascontiguousarray(geo.tri_pos().reshape(-1), np.float32)
+    rng = np.random.default_rng(11)
+    n = 3000
+    o = bmin + (bmax - bmin) * rng.random((n, 3), np.float32)
+    o[: n // 4] = bmin - (bmax - bmin) * 0.5 + (bmax - bmin) * 2.0 * rng.random((n // 4, 3), np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.ascontiguousarray(np.concatenate([o, d], axis=1), np.float32)
+    stats = np.zeros(2, np.uint64)
+    f = lambda a: a.ctypes.data_as(C.c_void_p)
+    emul.skip_check.restype = C.c_int
+    bad = emul.skip_check(f(bmin), f(bmax), f(r), f(cs), f(cells), f(pos), n, f(rays), f(stats))
+    assert bad == 0
+    assert stats[1] < stats[0] * 0.9, stats

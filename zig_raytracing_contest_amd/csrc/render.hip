@@ -92,7 +92,7 @@ struct TraceParams {
     // coarse-brick fields of the packed word (offset, width per axis) and
     // their in-brick bits; the 4^3-brick fields for OccX
     PackK pk;
-    const uint2* cells_v;
+    const uint32_t* cell32;   // 8 u32 per packed cell: begin, end, entry-face masks (see cell32_kernel)
     uint32_t occ_o1, occ_o2, occ_w0, occ_w1, occ_w2, occ_lowm;
     uint32_t ox1, ox2, ow0, ow1, ow2;
     float org[3], llc[3], right[3], up[3];
@@ -213,7 +213,7 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // [4] 64-wide rounds if each trip's tests were shared evenly.
 // PACKED: the walk state with the cell packed into one word (DdaV, grids of
 // at most 1024 cells per axis; same cells, same order, same t_exit), which
-// also indexes the cells (cells_v).
+// also indexes the cell records (cell32).
 template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
@@ -230,7 +230,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         bool occupied = brick_occupied_v(p, occ, s.pc);
         for (;;) {
             if (occupied) {
-                const uint2 cell = p.cells_v[s.pc];
+                const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
                 test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
             }
             bool crossed, exited;
@@ -775,8 +775,10 @@ constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 // register: the clobber is ignored), so nothing else in the park kernel may
 // rely on it: tests/test_codegen.py checks that every M0 access in its code
 // object is this sequence.
+// Range only (the segment's first cell: no cell was left, every ref is
+// tested; the caller writes the all-ones mask itself).
 __device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t pc, uint32_t* rng) {
-    const uint32_t* c = reinterpret_cast<const uint32_t*>(p.cells_v) + 2ull * pc;
+    const uint32_t* c = p.cell32 + 8ull * pc;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rng);
     // (an instruction offset would move the LDS destination too: the end
     // word gets its own address)
@@ -787,6 +789,38 @@ __device__ __forceinline__ void park_load_range(const TraceParams& p, uint32_t p
                  :
                  : "v"(c), "v"(c + 1), "s"(m0)
                  : "memory");
+}
+// Range and the mask of the refs to test for a ray that entered the cell
+// across `face` (cell32_kernel) into rng[lane], rng[64 + lane], rng[128 + lane].
+__device__ __forceinline__ void park_load_cell(const TraceParams& p, uint32_t pc, uint32_t face, uint32_t* rng) {
+    const uint32_t* c = p.cell32 + 8ull * pc;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rng);
+    asm volatile("s_mov_b32 m0, %3\n\t"
+                 "global_load_lds_dword %0, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %1, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %2, off"
+                 :
+                 : "v"(c), "v"(c + 1), "v"(c + 2 + face), "s"(m0)
+                 : "memory");
+}
+
+// Position of the r-th (from 0) set bit of m (r < popcount(m)): a binary
+// search over the halves' popcounts.
+__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t r) {
+    uint32_t pos = 0, c;
+    c = (uint32_t)__popc(m & 0xFFFFu);
+    if (r >= c) { r -= c; pos = 16u; }
+    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 8u));
+    if (r >= c) { r -= c; pos += 8u; }
+    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 4u));
+    if (r >= c) { r -= c; pos += 4u; }
+    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 2u));
+    if (r >= c) { r -= c; pos += 2u; }
+    c = __builtin_amdgcn_ubfe(m, pos, 1u);
+    if (r >= c) pos += 1u;
+    return pos;
 }
 
 // Per-wave LDS of the test rounds.
@@ -837,8 +871,8 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    __shared__ uint32_t s_rng[kParkWaves * 128];            // LDS-DMA range slots
-    uint32_t* const rng_slot = s_rng + 128u * (threadIdx.x >> 6);
+    __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
+    uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
     // OccX into LDS: (bits, prefix) entries, then the masks
     {
         const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
@@ -925,6 +959,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                                 ddav_from(s0, gk, pk, s);
                                 if (occx_cell(occx_mask(L, occx_brick(w, s)), s, pk)) {
                                     park_load_range(p, s.pc, rng_slot);
+                                    rng_slot[128 + lane] = ~0u;    // first cell: every ref
                                     st = kPark;
                                 } else {
                                     st = kWalk;
@@ -957,6 +992,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // chain of LDS latencies for two cells; the second step is
                 // speculative and dropped when the first cell parks or ends
                 // the segment (its lookup then reads a clamped brick)
+                const uint32_t pc0 = s.pc;
                 auto s1 = s;
                 bool cr1, cr2, ex1, ex2;
                 float te1, te2;
@@ -992,7 +1028,12 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 if (at1 ? d1 : d2) st = kDone;
                 DDAV_SEL(s, at1, s1, s2);
                 if (pkd) {                                         // one issue point per trip
-                    park_load_range(p, s.pc, rng_slot);
+                    // the face it entered across: the field the last step
+                    // changed, toward the axis's step sign (cell32_kernel)
+                    const uint32_t x = s.pc ^ (at1 ? pc0 : s1.pc);
+                    const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
+                                                      : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
+                    park_load_cell(p, s.pc, face, rng_slot);
                     st = kPark;
                 }
             }
@@ -1002,15 +1043,20 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         if (__ballot(st == kPark) != 0ull) {
             __builtin_amdgcn_s_waitcnt(0x3f70);                    // vmcnt(0): the ranges landed
             const bool ready = st == kPark;
-            const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane];
-            const uint32_t n = ready ? re - rb : 0u;
+            // the parked cell's refs still to test: those the mask keeps
+            // (cells of at most 32 refs; larger ones test every ref)
+            const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane], cnt = re - rb;
+            const uint32_t keep = cnt < 32u ? rng_slot[128 + lane] & ((1u << cnt) - 1u) : rng_slot[128 + lane];
+            const uint32_t n = ready ? (cnt <= 32u ? (uint32_t)__popc(keep) : cnt) : 0u;
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
             PARK_COUNT(5, 1);
             PARK_COUNT(6, (tot + 63u) / 64u);
             PARK_COUNT(7, tot);
             W.o[lane].w = nearest;
-            W.d[lane].w = __uint_as_float(rb - off);
+            rng_slot[lane] = rb;                                   // (the slots are free until the walk)
+            rng_slot[64 + lane] = off;
+            rng_slot[128 + lane] = cnt <= 32u ? keep : ~0u;
             W.best[lane] = ~0ull;
             uint32_t carry = 0;
             for (uint32_t r = 0; r < tot; r += 64u) {
@@ -1026,7 +1072,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 carry = (uint32_t)__builtin_amdgcn_readlane((int)owner, 63);
                 const uint32_t g = r + lane;
                 const float4 ro = W.o[owner], rd = W.d[owner];
-                const uint32_t j = __float_as_uint(rd.w) + g;
+                // pair g is the owner's (g - off)-th kept ref
+                const uint32_t kr = g - rng_slot[64 + owner];
+                const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit(rng_slot[128 + owner], kr) : kr);
                 bool cand = false;
                 float t = 0.0f, u = 0.0f, v = 0.0f;
                 if (g < tot) {
@@ -1098,15 +1146,18 @@ __device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx,
                grp, n_seg);
 }
 
-// LMATS: the material descriptors (at most kLdsMats) copied to LDS, so the
-// dependent chain hit -> triangle data -> material -> texels takes its
-// material hop from LDS instead of L2.
+// LMATS: the material descriptors (at most kLdsMats) copied to dynamic LDS
+// (nmat x 96 B: the shade kernel's LDS stays small, so its workgroups still
+// fit beside the other pass set's park kernel), so the dependent chain
+// hit -> triangle data -> material -> texels takes its material hop from LDS
+// instead of L2.
 constexpr uint32_t kLdsMats = 64;
 template <bool LMATS>
 __global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
-    __shared__ DevMat s_mats[LMATS ? kLdsMats : 1];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dynm[];    // LMATS: p.nmat DevMat
+    DevMat* const s_mats = reinterpret_cast<DevMat*>(s_dynm);
     for (uint32_t i = threadIdx.x; i < 514; i += blockDim.x) s_zig[i] = p.zig[i];
     if (LMATS)
         for (uint32_t i = threadIdx.x; i < p.nmat * (uint32_t)(sizeof(DevMat) / 4); i += blockDim.x)
@@ -1284,7 +1335,7 @@ constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that ru
 #endif
 constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
-constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 128 * 4 - 256;
+constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256;
 
 }  // namespace
 
@@ -1299,7 +1350,7 @@ struct zrt_context {
     // packed walks (DdaV): the layout and the cells indexed by the packed word
     PackK pk{};
     bool packed = false;
-    uint2* d_cells_v = nullptr;        // == d_cells for power-of-two grids, else a padded copy (owned)
+    uint32_t* d_cell32 = nullptr;      // cell records at the packed index (cell32_kernel)
     float* d_pos = nullptr;
     float4* d_data = nullptr;
     DevMat* d_mats = nullptr;
@@ -1422,7 +1473,7 @@ extern "C" int zrt_device_warmup(int device) {
 extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    if (c->d_cells_v && c->d_cells_v != c->d_cells) (void)hipFree(c->d_cells_v);
+    if (c->d_cell32) (void)hipFree(c->d_cell32);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
@@ -1526,39 +1577,84 @@ static int context_base(zrt_context* c) {
 static int context_materials(zrt_context* c, const zrt_scene* s);
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells);
 
-// The cells at their packed-word index (x | y << o1 | z << o2) in a grid
-// padded to powers of two per axis; the padding stays {0, 0} (empty).
-__global__ __launch_bounds__(kBlock) void cells_pad_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
-                                                           uint32_t ncells, uint32_t o1, uint32_t o2,
-                                                           uint2* __restrict__ out) {
+// Word i of ref k's (v0, e1, e2) in the context's triangle layout.
+__device__ __forceinline__ uint32_t tri_word(const float* pos, uint32_t k, uint32_t i) {
+    return __float_as_uint(pos[(uint64_t)kTriFloats * k + (kTriFloats == 9 ? i : i + i / 3)]);
+}
+__device__ __forceinline__ bool same_tri(const float* pos, uint32_t a, uint32_t b) {
+    for (uint32_t i = 0; i < 9; ++i)
+        if (tri_word(pos, a, i) != tri_word(pos, b, i)) return false;
+    return true;
+}
+
+// The packed walks' cell records: 8 u32 per cell at its packed-word index
+// (x | y << o1 | z << o2; the padding of a non-power-of-two grid stays empty):
+// begin, end, then for each entry face f = 2 * axis + (the ray steps toward
+// -axis) the mask of the refs (bit k: ref begin + k) that a ray entering the
+// cell across f must still test.
+//
+// A ray enters a cell only from the cell it has just left, across the face
+// they share, and leaves a cell only after testing all of its refs
+// (stage3.zig:164-182).  A ref whose (v0, e1, e2) bits equal those of a ref
+// of that neighbour gives the same (hit, t, u, v) as the one already tested
+// there: if that one was taken, nearest == t and `nearest > t` fails; if not,
+// nearest has only shrunk since.  So skipping it changes no hit, no tie
+// (ties resolve within the cell by ref order, and the kept refs keep their
+// order and index) and no break test.  Refs of cells with more than 32 refs
+// are all kept (mask all ones), and so are those of a face on the grid
+// boundary (no ray steps in across it).  About half of all triangle tests on
+// the contest stand-in repeat the previous cell's (triangles span ~5.6
+// cells), a third on the Sponza-scale one.
+__global__ __launch_bounds__(kBlock) void cell32_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                        uint32_t r2, uint32_t ncells, uint32_t o1, uint32_t o2,
+                                                        const float* __restrict__ pos, uint32_t* __restrict__ out) {
     for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint2 c = cells[ci];
         const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / r0 / r1;
-        out[x | (y << o1) | (z << o2)] = cells[ci];
+        uint32_t* rec = out + 8ull * (x | (y << o1) | (z << o2));
+        rec[0] = c.x;
+        rec[1] = c.y;
+        const uint32_t n = c.y - c.x;
+        const uint32_t all = n >= 32u ? ~0u : (1u << n) - 1u;
+        for (uint32_t f = 0; f < 6; ++f) {
+            const uint32_t axis = f >> 1, toward_neg = f & 1u;
+            const uint32_t cc = axis == 0 ? x : (axis == 1 ? y : z), rr = axis == 0 ? r0 : (axis == 1 ? r1 : r2);
+            // the cell left: one step back against the ray's direction
+            const bool inside = toward_neg ? cc + 1u < rr : cc > 0u;
+            uint32_t m = all;
+            if (inside && n > 0u && n <= 32u) {
+                const uint32_t step = axis == 0 ? 1u : (axis == 1 ? r0 : r0 * r1);
+                const uint2 pc = cells[toward_neg ? ci + step : ci - step];
+                for (uint32_t k = 0; k < n; ++k)
+                    for (uint32_t q = pc.x; q < pc.y; ++q)
+                        if (same_tri(pos, c.x + k, q)) {
+                            m &= ~(1u << k);
+                            break;
+                        }
+            }
+            rec[2 + f] = m;
+        }
     }
 }
 
-// The packed walks' layout (DdaV) and, for a grid whose resolution is not a
-// power of two per axis, the padded copy of the cells it indexes (none beyond
-// 16 GiB, or beyond 256 MiB and 16x the cells -- flat grids whose narrow
-// axis pack_layout widened: such a grid walks unpacked).
-constexpr uint64_t kPadCellsMax = 16ull << 30;
+// The packed walks' layout (DdaV) and their cell records (cell32_kernel;
+// none beyond 16 GiB, or beyond 1 GiB and 16x the cells' own 8 B -- flat
+// grids whose narrow axis pack_layout widened: such a grid walks unpacked).
+constexpr uint64_t kCell32Max = 16ull << 30;
 static int context_packed(zrt_context* c) {
     const uint32_t* r = c->grid.resolution;
     c->packed = pack_layout(r, c->pk);
     if (!c->packed) return ZRT_OK;
-    if (pack_is_linear(r, c->pk)) {
-        c->d_cells_v = c->d_cells;
-        return ZRT_OK;
-    }
     const uint64_t n = 1ull << (c->pk.b0 + c->pk.b1 + c->pk.b2);
-    if (8 * n > kPadCellsMax || (n > 16ull * c->ncells && 8 * n > (256ull << 20))) {
+    if (32 * n > kCell32Max || (n > 16ull * c->ncells && 32 * n > (1ull << 30))) {
         c->packed = false;
         return ZRT_OK;
     }
-    HIP_TRY(hipMalloc((void**)&c->d_cells_v, 8 * n));
-    HIP_TRY(hipMemsetAsync(c->d_cells_v, 0, 8 * n, c->stream));
-    hipLaunchKernelGGL(cells_pad_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells,
-                       c->pk.o1, c->pk.o2, c->d_cells_v);
+    HIP_TRY(hipMalloc((void**)&c->d_cell32, 32 * n));
+    if (!pack_is_linear(r, c->pk)) HIP_TRY(hipMemsetAsync(c->d_cell32, 0, 32 * n, c->stream));
+    hipLaunchKernelGGL(cell32_kernel, dim3(std::min<uint32_t>((c->ncells + kBlock - 1) / kBlock, 16384)), dim3(kBlock),
+                       0, c->stream, c->d_cells, r[0], r[1], r[2], c->ncells, c->pk.o1, c->pk.o2, c->d_pos,
+                       c->d_cell32);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
     return ZRT_OK;
@@ -2103,6 +2199,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
+    const size_t lds_shade = c->nmat <= kLdsMats ? c->nmat * sizeof(DevMat) : 0;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
         if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
 
@@ -2167,7 +2264,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     } else {
         if ((rc = grid_for((const void*)f_first, thr_first, lds_first, &grid_first)) != ZRT_OK) return rc;
         if ((rc = grid_for((const void*)f_next, thr_next, lds_next, &grid_next)) != ZRT_OK) return rc;
-        if ((rc = grid_for((const void*)s_next, kTraceThreads, 0, &grid_shade)) != ZRT_OK) return rc;
+        if ((rc = grid_for((const void*)s_next, kTraceThreads, lds_shade, &grid_shade)) != ZRT_OK) return rc;
     }
 
     TraceParams tp;
@@ -2184,7 +2281,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
     tp.cells = c->d_cells;
     tp.pk = c->pk;
-    tp.cells_v = c->d_cells_v;
+    tp.cell32 = c->d_cell32;
     {
         const uint32_t sh = c->occ_shift, b[3] = {c->pk.b0, c->pk.b1, c->pk.b2};
         auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
@@ -2297,7 +2394,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 ++kp.launches[cls];
                 if (k > 0 && park_next) {                    // same bounce, shading half
                     if ((rc = kt_begin(ZRT_KERNEL_SHADE, sm)) != ZRT_OK) return rc;
-                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), 0, sm, W);
+                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), lds_shade, sm, W);
                     HIP_TRY(hipGetLastError());
                     if ((rc = kt_end(sm)) != ZRT_OK) return rc;
                     ++kp.launches[ZRT_KERNEL_SHADE];
