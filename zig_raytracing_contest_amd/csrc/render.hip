@@ -70,6 +70,10 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
+// DDA steps per park walk trip (every cell's brick lookup in flight at once)
+#ifndef ZRT_WALK_STEPS
+#define ZRT_WALK_STEPS 2
+#endif
 constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
 struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -992,6 +996,54 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // chain of LDS latencies for two cells; the second step is
                 // speculative and dropped when the first cell parks or ends
                 // the segment (its lookup then reads a clamped brick)
+#if ZRT_WALK_STEPS > 2
+                // ZRT_WALK_STEPS DDA steps per trip, every cell's lookup in
+                // flight before any is used; the trip ends in the first cell
+                // that ends the segment or holds triangles (steps after it
+                // are speculative and dropped)
+                constexpr int kS = ZRT_WALK_STEPS;
+                DdaV ss[kS];
+                bool ex[kS], dd[kS], oo[kS];
+                float te[kS];
+                unsigned long long q[kS];
+#pragma unroll
+                for (int k = 0; k < kS; ++k) {
+                    ss[k] = k ? ss[k - 1] : s;
+                    bool cr;
+                    PARK_STEP(ss[k], cr, ex[k], te[k]);
+                    (void)cr;
+                }
+#pragma unroll
+                for (int k = 0; k < kS; ++k) q[k] = occx_mask_clamped(L, occx_brick(w, ss[k]), w.occx_nbw);
+#pragma unroll
+                for (int k = 0; k < kS; ++k) asm volatile("" : "+v"(q[k]));
+#pragma unroll
+                for (int k = 0; k < kS; ++k) {
+                    dd[k] = ex[k] || nearest <= te[k];
+                    oo[k] = occx_cell(q[k], ss[k], pk);
+                }
+                // from the last step back to the first: the first stopping step wins
+                DdaV sel = ss[kS - 1];
+                uint32_t prev = ss[kS - 2].pc;
+                bool pkd = false, dn = false;
+#pragma unroll
+                for (int k = kS - 1; k >= 0; --k) {
+                    const bool stop = dd[k] || oo[k];
+                    DDAV_SEL(sel, stop, ss[k], sel);
+                    prev = stop ? (k ? ss[k - 1].pc : s.pc) : prev;
+                    pkd = stop ? !dd[k] : pkd;
+                    dn = stop ? dd[k] : dn;
+                }
+                if (dn) st = kDone;
+                s = sel;
+                if (pkd) {
+                    const uint32_t x = s.pc ^ prev;
+                    const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
+                                                      : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
+                    park_load_cell(p, s.pc, face, rng_slot);
+                    st = kPark;
+                }
+#else
                 const uint32_t pc0 = s.pc;
                 auto s1 = s;
                 bool cr1, cr2, ex1, ex2;
@@ -1036,6 +1088,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     park_load_cell(p, s.pc, face, rng_slot);
                     st = kPark;
                 }
+#endif
             }
         }
         PARK_STAMP(1);
@@ -1153,7 +1206,10 @@ __device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx,
 // instead of L2.
 constexpr uint32_t kLdsMats = 64;
 template <bool LMATS>
-__global__ __launch_bounds__(kTraceBlock) void wf_shade_kernel(const WfParams w) {
+#ifndef ZRT_SHADE_MINW
+#define ZRT_SHADE_MINW 1
+#endif
+__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dynm[];    // LMATS: p.nmat DevMat
