@@ -114,25 +114,25 @@ def _loops(ins):
 
 
 def test_park_walk_trip_is_not_a_register_shuffle(code):
-    """The walk trip (two DDA steps, two OccX lookups = 4 LDS reads, one range
-    DMA issue point) stays ~115 VALU (143 before the packed cell, 130 before
-    the opaque third-axis select, 123 with a brick-mask select).  Its old branchy form let the compiler
-    copy the whole walk state through every join: a one-line change elsewhere
-    in the kernel took it from 160 to 232 VALU (96 v_mov) and cfg3 lost 2-3%
-    with identical images."""
+    """The walk trip (ZRT_WALK_STEPS = 4 DDA steps, four OccX lookups = 8 LDS
+    reads, one range DMA issue point) stays ~202 VALU (round 2's two-step trip
+    was 115, round 3's 76 before the trip grew to four steps).  Its old branchy
+    form let the compiler copy the whole walk state through every join: a
+    one-line change elsewhere in the kernel took it from 160 to 232 VALU (96
+    v_mov) and cfg3 lost 2-3% with identical images."""
     sc, ks = code
     ins = _kernel(ks, "wf_park_kernel")
     trips = []
     for b, e in _loops(ins):
         body = [t.strip() for _, t in ins[b:e + 1]]
-        if sum(t.startswith("ds_read") for t in body) == 4 and not any(t.startswith("ds_write") for t in body) \
+        if sum(t.startswith("ds_read") for t in body) == 8 and not any(t.startswith("ds_write") for t in body) \
                 and any(t.startswith("global_load_lds") for t in ins_after(ins, e)):
             trips.append(body)
     assert trips, "walk loop not found"
     body = min(trips, key=len)
     valu = sum(t.startswith("v_") for t in body)
     movs = sum(t.startswith("v_mov") for t in body)
-    assert valu <= 170 and movs <= 40, (valu, movs)
+    assert valu <= 240 and movs <= 40, (valu, movs)
 
 
 def ins_after(ins, e, n=40):

@@ -70,9 +70,11 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
-// DDA steps per park walk trip (every cell's brick lookup in flight at once)
+// DDA steps per park walk trip, every cell's brick lookup in flight at once
+// (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
+// +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
 #ifndef ZRT_WALK_STEPS
-#define ZRT_WALK_STEPS 2
+#define ZRT_WALK_STEPS 4
 #endif
 constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
 struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
@@ -996,12 +998,12 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // chain of LDS latencies for two cells; the second step is
                 // speculative and dropped when the first cell parks or ends
                 // the segment (its lookup then reads a clamped brick)
-#if ZRT_WALK_STEPS > 2
                 // ZRT_WALK_STEPS DDA steps per trip, every cell's lookup in
                 // flight before any is used; the trip ends in the first cell
                 // that ends the segment or holds triangles (steps after it
                 // are speculative and dropped)
                 constexpr int kS = ZRT_WALK_STEPS;
+                static_assert(kS >= 2, "the trip keeps the cell before its last step");
                 DdaV ss[kS];
                 bool ex[kS], dd[kS], oo[kS];
                 float te[kS];
@@ -1043,52 +1045,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     park_load_cell(p, s.pc, face, rng_slot);
                     st = kPark;
                 }
-#else
-                const uint32_t pc0 = s.pc;
-                auto s1 = s;
-                bool cr1, cr2, ex1, ex2;
-                float te1, te2;
-                PARK_STEP(s1, cr1, ex1, te1);
-                auto s2 = s1;
-                PARK_STEP(s2, cr2, ex2, te2);
-                unsigned long long q1 = occx_mask_clamped(L, occx_brick(w, s1), w.occx_nbw);
-                unsigned long long q2 = occx_mask_clamped(L, occx_brick(w, s2), w.occx_nbw);
-                // both lookups complete here, ahead of the selects below
-                // (left alone, the compiler sinks the second into the branch
-                // that uses it and the two LDS chains run one after the other)
-                asm volatile("" : "+v"(q1), "+v"(q2));
-                // a cell's lookup is its brick's mask whether or not the step
-                // crossed into a new brick (uncrossed: the same brick, the
-                // same mask), so the walk keeps no current-brick mask and
-                // selects nothing on the crossing (r02f3: 115 instead of 123
-                // VALU per trip); a step past the grid exit reads a clamped
-                // brick, but that step ends the segment (T_EXIT = +inf) and
-                // its mask is never tested
-                (void)cr1;
-                (void)cr2;
-                const unsigned long long m1 = q1;
-                const unsigned long long m2 = q2;
-                // the trip ends in the first of its cells that ends the
-                // segment (stage3.zig:179-182) or holds triangles; selects,
-                // not branches: the branchy form made the compiler copy the
-                // whole state through every join (up to 232 VALU per trip)
-                // traceRay's break test nearest <= T_EXIT, T_EXIT = +inf at the exit
-                const bool d1 = ex1 || nearest <= te1, d2 = ex2 || nearest <= te2;
-                const bool o1 = occx_cell(m1, s1, pk), o2 = occx_cell(m2, s2, pk);
-                const bool at1 = d1 || o1;
-                const bool pkd = at1 ? !d1 : (!d2 && o2);
-                if (at1 ? d1 : d2) st = kDone;
-                DDAV_SEL(s, at1, s1, s2);
-                if (pkd) {                                         // one issue point per trip
-                    // the face it entered across: the field the last step
-                    // changed, toward the axis's step sign (cell32_kernel)
-                    const uint32_t x = s.pc ^ (at1 ? pc0 : s1.pc);
-                    const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
-                                                      : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
-                    park_load_cell(p, s.pc, face, rng_slot);
-                    st = kPark;
-                }
-#endif
             }
         }
         PARK_STAMP(1);
