@@ -31,7 +31,7 @@ import json
 import os
 import re
 
-KERNELS = (("wf_park_kernel", r"wf_park_kernel"), ("wf_shade_kernel", r"wf_shade_kernel"),
+KERNELS = (("wf_park_kernel", r"wf_park2?_kernel"), ("wf_shade_kernel", r"wf_shade_kernel"),
            ("wf_kernel (primary)", r"wf_kernel<\d+, true"), ("wf_kernel (bounce)", r"wf_kernel<\d+, false"),
            ("wf_resolve_kernel", r"wf_resolve_kernel"), ("trace_kernel", r"trace_kernel"))
 
