@@ -60,7 +60,9 @@ static uint64_t g_walk_fails = 0, g_walk_steps = 0;
 // packed word equals the cell's packing (and, on power-of-two grids, the
 // linear index), the crossing flag, T_EXIT = EXITED ? +inf : TC and the ts bit
 // for bit up to the exit step (past it the packed fields may carry; the walk
-// has ended there), and the in-brick index of the park walk's OccX test.
+// has ended there), and the in-brick index of the park walk's OccX test;
+// DDAV_STEPM / DDAV_STEPMB (the same step on lane masks) must equal
+// DDAV_STEPX bit for bit.
 static void walk_w(const GridK& k, Dda s) {
     DdaW w;
     ddaw_from(s, k, w);
@@ -71,12 +73,29 @@ static void walk_w(const GridK& k, Dda s) {
     const bool linear = pack_is_linear(res, pk);
     DdaV x;
     ddav_from(s, k, pk, x);
+    DdaV y = x;                              // DDAV_STEPM (lane-mask form of the park walk trip)
+    DdaV z = x;                              // DDAV_STEPMB (its lane-walk form)
     for (int guard = 0; guard < 100000; ++guard) {
         bool c1, c2, c4, ex4;
         float e1, e2, tc4;
+        const uint32_t pc_before = x.pc;
         DDA_STEP(s, k, 2, c1, e1);
         DDAW_STEP(w, 2, c2, e2);
         DDAV_STEPX(x, pk, pk.low2, c4, ex4, tc4);
+        LaneM ex5;
+        float tc5;
+        const bool y_in_step = y.pc == pc_before;
+        DDAV_STEPM(y, pk.f0, pk.f1, pk.f2, ex5, tc5);
+        bool c6, ex6;
+        float tc6;
+        DDAV_STEPMB(z, pk.f0, pk.f1, pk.f2, pk.low2, c6, ex6, tc6);
+        if (!y_in_step || ex5 != ex4 || memcmp(&tc5, &tc4, 4) || y.pc != x.pc || memcmp(&y.tn0, &x.tn0, 4) ||
+            memcmp(&y.tn1, &x.tn1, 4) || memcmp(&y.tn2, &x.tn2, 4) || c6 != c4 || ex6 != ex4 ||
+            memcmp(&tc6, &tc4, 4) || z.pc != x.pc || memcmp(&z.tn0, &x.tn0, 4) || memcmp(&z.tn1, &x.tn1, 4) ||
+            memcmp(&z.tn2, &x.tn2, 4)) {
+            ++g_walk_fails;
+            return;
+        }
         ++g_walk_steps;
         const bool same = c1 == c2 && !memcmp(&e1, &e2, 4) && s.c0 == w.c0 && s.c1 == w.c1 && s.c2 == w.c2 &&
                           s.lin == w.lin && !memcmp(&s.tn0, &w.tn0, 4) && !memcmp(&s.tn1, &w.tn1, 4) &&

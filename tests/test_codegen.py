@@ -115,8 +115,9 @@ def _loops(ins):
 
 def test_park_walk_trip_is_not_a_register_shuffle(code):
     """The walk trip (ZRT_WALK_STEPS = 4 DDA steps, four OccX lookups = 8 LDS
-    reads, one range DMA issue point) stays ~202 VALU (round 2's two-step trip
-    was 115, round 3's 76 before the trip grew to four steps).  Its old branchy
+    reads, one range DMA issue point) stays ~179 VALU (202 before its
+    booleans became lane masks; round 2's two-step trip was 115, round 3's 76
+    before the trip grew to four steps).  Its old branchy
     form let the compiler copy the whole walk state through every join: a
     one-line change elsewhere in the kernel took it from 160 to 232 VALU (96
     v_mov) and cfg3 lost 2-3% with identical images."""
@@ -132,7 +133,28 @@ def test_park_walk_trip_is_not_a_register_shuffle(code):
     body = min(trips, key=len)
     valu = sum(t.startswith("v_") for t in body)
     movs = sum(t.startswith("v_mov") for t in body)
-    assert valu <= 240 and movs <= 40, (valu, movs)
+    assert valu <= 200 and movs <= 10, (valu, movs)
+    # the trip's selects are v_cndmask on lane masks (DDAV_STEPM): no execz
+    # branch around a select inside the trip (round 3's per-lane booleans put
+    # four there, each with its own exec save/restore)
+    inner = [t for t in body[:-1] if t.startswith("s_cbranch_execz")]
+    assert len(inner) <= 2, inner
+
+
+def test_walk_loops_load_nothing_from_the_kernel_arguments(code):
+    """A select between kernel-argument fields (the packed walk's field masks
+    f0/f1/f2) became, in round 3's primary lane walk, a vector load from the
+    kernel-argument segment at a selected offset, waited on by a vmcnt(0) in
+    every DDA step; the fields are laundered into registers now.  No timed
+    kernel may form a vector address from the kernel-argument pointer
+    (s[0:1] at entry) inside a loop."""
+    import re
+    sc, ks = code
+    for sub in sc.timed():
+        ins = _kernel(ks, sub)
+        for b, e in _loops(ins):
+            bad = [t.strip() for _, t in ins[b:e + 1] if re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", t)]
+            assert not bad, (sub, bad[:2])
 
 
 def ins_after(ins, e, n=40):

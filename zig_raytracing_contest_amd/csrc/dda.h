@@ -289,6 +289,75 @@ ZHD float opaque_f(float x) {
         (S).tn2 = a0_ ? t2_ : (a1_ ? opaque_f(t2_) : un_);    /* a2: neither */       \
         (S).pc = pn_;                                                                \
     } while (0)
+// Lane masks for the park walk trip.  On the device a LaneM is the wave's
+// 64-bit lane mask (a ballot, i.e. the compare result in an SGPR pair) and
+// lm_sel is one v_cndmask_b32 on it, so the compiler can neither turn a
+// select's condition into booleans materialised in VGPRs nor wrap a select
+// in a branch (the r03k ISA of DDAV_STEPX: 4 execz branches and 8
+// SGPR-to-VGPR copies per four-step trip).  On the host (the step check in
+// tests/cpp/dda_skip_check.cpp) a LaneM is one lane's bool: same booleans,
+// same selects.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint64_t LaneM;
+__device__ __forceinline__ LaneM lm_of(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ LaneM lm_and(LaneM a, LaneM b) { return a & b; }
+__device__ __forceinline__ LaneM lm_andn(LaneM a, LaneM b) { return a & ~b; }
+__device__ __forceinline__ LaneM lm_or(LaneM a, LaneM b) { return a | b; }
+__device__ __forceinline__ float lm_sel(LaneM m, float t, float f) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+#else
+typedef bool LaneM;
+ZHD LaneM lm_of(bool c) { return c; }
+ZHD LaneM lm_and(LaneM a, LaneM b) { return a && b; }
+ZHD LaneM lm_andn(LaneM a, LaneM b) { return a && !b; }
+ZHD LaneM lm_or(LaneM a, LaneM b) { return a || b; }
+ZHD float lm_sel(LaneM m, float t, float f) { return m ? t : f; }
+ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
+#endif
+// DDAV_STEPX on lane masks: A0 = t0<t1 && t0<t2, A1 = !(t0<t1) && t1<t2,
+// else axis 2 (DDA_STEP's booleans); FV0..FV2: the field masks (in VGPRs
+// for the park walk: a select between two SGPR operands needs a copy
+// first).  The core selects the step's axis quantities and updates the
+// crossing ts; FM: the axis's field mask, DP: its packed cell step.
+#define DDAV_STEPM_CORE(S, FV0, FV1, FV2, FM, DP, TC)                                \
+    const float t0_ = (S).tn0, t1_ = (S).tn1, t2_ = (S).tn2;                         \
+    const LaneM m01_ = lm_of(t0_ < t1_), m02_ = lm_of(t0_ < t2_), m12_ = lm_of(t1_ < t2_); \
+    const LaneM a0_ = lm_and(m01_, m02_);                                            \
+    const LaneM a1_ = lm_andn(m12_, m01_);                                           \
+    const LaneM a01_ = lm_or(a0_, a1_);                                              \
+    const float tc_ = lm_sel(a0_, t0_, lm_sel(a1_, t1_, t2_));                       \
+    const float dt_ = lm_sel(a0_, (S).td0, lm_sel(a1_, (S).td1, (S).td2));           \
+    const uint32_t FM = lm_selu(a0_, (FV0), lm_selu(a1_, (FV1), (FV2)));             \
+    const uint32_t DP = lm_selu(a0_, (S).d0, lm_selu(a1_, (S).d1, (S).d2));          \
+    (TC) = tc_;                                                                      \
+    const float un_ = tc_ + dt_;                                                     \
+    (S).tn0 = lm_sel(a0_, un_, t0_);                                                 \
+    (S).tn1 = lm_sel(a1_, un_, t1_);                                                 \
+    (S).tn2 = lm_sel(a01_, t2_, un_);
+// EXM: the lane mask of the lanes whose step's axis is at its exit cell
+#define DDAV_STEPM(S, FV0, FV1, FV2, EXM, TC)                                        \
+    do {                                                                             \
+        DDAV_STEPM_CORE(S, FV0, FV1, FV2, fm_, dp_, TC)                              \
+        (EXM) = lm_of((((S).pc ^ (S).pe) & fm_) == 0u);                              \
+        (S).pc += dp_;                                                               \
+    } while (0)
+// The same with DDAV_STEPX's per-lane outputs (the lane walk)
+#define DDAV_STEPMB(S, FV0, FV1, FV2, LOWM, CROSSED, EXITED, TC)                     \
+    do {                                                                             \
+        DDAV_STEPM_CORE(S, FV0, FV1, FV2, fm_, dp_, TC)                              \
+        const uint32_t pn_ = (S).pc + dp_;                                           \
+        (CROSSED) = (((S).pc ^ pn_) & ~(LOWM)) != 0u;                                \
+        (EXITED) = (((S).pc ^ (S).pe) & fm_) == 0u;                                  \
+        (S).pc = pn_;                                                                \
+    } while (0)
 #define DDAV_SEL(D, C, A, B)                                                          \
     do {                                                                             \
         (D).tn0 = (C) ? (A).tn0 : (B).tn0; (D).tn1 = (C) ? (A).tn1 : (B).tn1;        \

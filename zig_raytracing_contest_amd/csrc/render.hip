@@ -233,6 +233,12 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         static_assert(!STATS, "the counting build walks unpacked");
         DdaV s;
         ddav_from(s0, gk, p.pk, s);
+        // the field masks as laundered registers: selected straight from the
+        // kernel arguments they became a vector load at a selected offset
+        // (v_cndmask of 0x94/0x98/0x9c, global_load_dword, vmcnt(0)) in
+        // every step (r03 ISA)
+        uint32_t f0 = p.pk.f0, f1 = p.pk.f1, f2 = p.pk.f2;
+        asm("" : "+s"(f0), "+s"(f1), "+s"(f2));
         bool occupied = brick_occupied_v(p, occ, s.pc);
         for (;;) {
             if (occupied) {
@@ -241,7 +247,9 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             }
             bool crossed, exited;
             float tc;
-            DDAV_STEPX(s, p.pk, p.occ_lowm, crossed, exited, tc);
+            PackK pkl = p.pk;
+            pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
+            DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
@@ -906,7 +914,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     DdaV s;                                // grids of <= 1024 cells per axis (zrt_context_render)
     const PackK pk = p.pk;
-#define PARK_STEP(S, CR, EX, TC) DDAV_STEPX(S, pk, pk.low2, CR, EX, TC)
+    uint32_t fv0 = pk.f0, fv1 = pk.f1, fv2 = pk.f2;        // field masks in VGPRs (DDAV_STEPM)
+    asm("" : "+v"(fv0), "+v"(fv1), "+v"(fv2));
     memset(&s, 0, sizeof s);
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
@@ -993,27 +1002,24 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             PARK_COUNT(3, 1);
             PARK_COUNT(4, __popcll(wk));
             if (st == kWalk) {
-                // two DDA steps per trip: both cells' brick lookups are
-                // issued before either is used, so the trip waits out one
-                // chain of LDS latencies for two cells; the second step is
-                // speculative and dropped when the first cell parks or ends
-                // the segment (its lookup then reads a clamped brick)
                 // ZRT_WALK_STEPS DDA steps per trip, every cell's lookup in
                 // flight before any is used; the trip ends in the first cell
                 // that ends the segment or holds triangles (steps after it
-                // are speculative and dropped)
+                // are speculative and dropped; their lookups read a clamped
+                // brick).  Every boolean of the trip is a lane mask and every
+                // select one v_cndmask on it (DDAV_STEPM: 179 VALU and no
+                // branch per four-step trip, against 202 VALU, 14 v_mov and
+                // four execz branches with per-lane booleans, r03p)
                 constexpr int kS = ZRT_WALK_STEPS;
                 static_assert(kS >= 2, "the trip keeps the cell before its last step");
                 DdaV ss[kS];
-                bool ex[kS], dd[kS], oo[kS];
+                LaneM ex[kS], stop[kS], dd[kS];
                 float te[kS];
                 unsigned long long q[kS];
 #pragma unroll
                 for (int k = 0; k < kS; ++k) {
                     ss[k] = k ? ss[k - 1] : s;
-                    bool cr;
-                    PARK_STEP(ss[k], cr, ex[k], te[k]);
-                    (void)cr;
+                    DDAV_STEPM(ss[k], fv0, fv1, fv2, ex[k], te[k]);
                 }
 #pragma unroll
                 for (int k = 0; k < kS; ++k) q[k] = occx_mask_clamped(L, occx_brick(w, ss[k]), w.occx_nbw);
@@ -1021,24 +1027,27 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 for (int k = 0; k < kS; ++k) asm volatile("" : "+v"(q[k]));
 #pragma unroll
                 for (int k = 0; k < kS; ++k) {
-                    dd[k] = ex[k] || nearest <= te[k];
-                    oo[k] = occx_cell(q[k], ss[k], pk);
+                    dd[k] = lm_or(ex[k], lm_of(nearest <= te[k]));
+                    stop[k] = lm_or(dd[k], lm_of(occx_cell(q[k], ss[k], pk)));
                 }
-                // from the last step back to the first: the first stopping step wins
+                // the first stopping step wins: from the last step back (the
+                // last step's selects are identities)
                 DdaV sel = ss[kS - 1];
                 uint32_t prev = ss[kS - 2].pc;
-                bool pkd = false, dn = false;
+                LaneM pkd = lm_andn(stop[kS - 1], dd[kS - 1]), dn = dd[kS - 1];
 #pragma unroll
-                for (int k = kS - 1; k >= 0; --k) {
-                    const bool stop = dd[k] || oo[k];
-                    DDAV_SEL(sel, stop, ss[k], sel);
-                    prev = stop ? (k ? ss[k - 1].pc : s.pc) : prev;
-                    pkd = stop ? !dd[k] : pkd;
-                    dn = stop ? dd[k] : dn;
+                for (int k = kS - 2; k >= 0; --k) {
+                    sel.tn0 = lm_sel(stop[k], ss[k].tn0, sel.tn0);
+                    sel.tn1 = lm_sel(stop[k], ss[k].tn1, sel.tn1);
+                    sel.tn2 = lm_sel(stop[k], ss[k].tn2, sel.tn2);
+                    sel.pc = lm_selu(stop[k], ss[k].pc, sel.pc);
+                    prev = lm_selu(stop[k], k ? ss[k - 1].pc : s.pc, prev);
+                    pkd = lm_or(lm_andn(pkd, stop[k]), lm_andn(stop[k], dd[k]));
+                    dn = lm_or(lm_andn(dn, stop[k]), dd[k]);
                 }
-                if (dn) st = kDone;
+                st = lm_selu(dn, kDone, st);
                 s = sel;
-                if (pkd) {
+                if (lm_selu(pkd, 1u, 0u)) {
                     const uint32_t x = s.pc ^ prev;
                     const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
                                                       : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
@@ -1113,7 +1122,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         PARK_STAMP(2);
     }
     __builtin_amdgcn_s_waitcnt(0x3f70);                            // vmcnt(0): no LDS-DMA outlives the wave
-#undef PARK_STEP
 #ifdef ZRT_SWEEP
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
