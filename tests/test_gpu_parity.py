@@ -189,12 +189,18 @@ def test_probe_texture(oracle_mod, rng):
         tex = rng.uniform(0, 1, w * h * chans).astype(np.float32)
         lim = (0, w - 1, 0, h - 1) if clamp else (-2**31, 2**31 - 1, -2**31, 2**31 - 1)
         aux = np.concatenate([np.array([chans, w, h, *lim, 0], np.int32).view(np.float32), tex])
-        uv = np.concatenate([rng.uniform(-3, 3, (500, 2)),
-                             np.array([[0, 0], [1, 1], [0.5, -0.5], [-1e-7, 2.0]])]).astype(np.float32)
+        # coordinates inside the image, repeats (the device modulo's float
+        # quotient below 2^21 texels, its integer division above), and the
+        # saturating @intFromFloat edges (NaN, +-inf, beyond int32)
+        edge = [0, 1, 0.5, -0.5, -1e-7, 2.0, 1000.3, -1000.7, 3e5, -3e5, 4.1e5, 1e6, -1e6, 2e8, -2e8,
+                4.3e8, -4.3e8, 1e30, -1e30, np.inf, -np.inf, np.nan]
+        uv = np.concatenate([rng.uniform(-3, 3, (500, 2)), rng.uniform(-5e5, 5e5, (200, 2)),
+                             np.array([[a, b] for a in edge for b in (edge[0], edge[7], edge[-1])] +
+                                      [[b, a] for a in edge for b in (edge[2], edge[11])])]).astype(np.float32)
         out = native.probe(native.PROBE_TEXTURE, uv, len(uv), (len(uv), 3), aux=aux)
         for i, (u, v) in enumerate(uv):
             e = oracle_mod.tex_sample(tex, chans, w, h, *lim, u, v)
-            assert np.array_equal(out[i, :chans], e), (i, u, v)
+            assert np.array_equal(out[i, :chans], e, equal_nan=True), (i, u, v)
 
 
 CASES = [("sphere", None, 64, 64, 4), ("cornell", None, 64, 64, 8),

@@ -45,17 +45,18 @@ ZHD v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 
 // @intFromFloat f32 -> u32 / i32, defined (saturating) where the reference
 // is UB; the oracle uses the same definition (oracle/zrt_oracle.c f2u/f2i).
+// Written as selects around one in-range conversion (4294967040 and
+// 2147483520 are the largest floats below 2^32 and 2^31): with early returns
+// the compiler nested three execz branches around every conversion.
 ZHD uint32_t f2u(float f) {
-    if (!(f > -1.0f)) return 0u;
-    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
-    if (f < 0.0f) return 0u;
-    return (uint32_t)f;
+    const uint32_t c = (uint32_t)fminf(fmaxf(f, 0.0f), 4294967040.0f);
+    const uint32_t s = f >= 4294967296.0f ? 0xFFFFFFFFu : c;
+    return f > -1.0f ? s : 0u;
 }
 ZHD int32_t f2i(float f) {
-    if (f != f) return 0;
-    if (f >= 2147483648.0f) return 2147483647;
-    if (f <= -2147483648.0f) return (int32_t)0x80000000u;
-    return (int32_t)f;
+    const int32_t c = (int32_t)fminf(fmaxf(f, -2147483648.0f), 2147483520.0f);
+    const int32_t s = f >= 2147483648.0f ? 2147483647 : c;
+    return f != f ? 0 : s;
 }
 
 // ---- Bbox / Grid (linalg.zig:294-469) ------------------------------------
@@ -332,7 +333,25 @@ ZHD bool tri_ray_flat(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, floa
 // ---- textures (stage3.zig:94-121) -----------------------------------------
 ZHD float tex_frac(float v) { return fabsf(v - truncf(v)); }
 ZHD int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
-ZHD int32_t fmod_i(int32_t a, int32_t b) { const int32_t r = a % b; return r < 0 ? r + b : r; }
+// @mod(a, b) for b > 0 (texture extents).  On the device, a in [0, b) --
+// texture coordinates inside the image -- returns a, and |a| < 2^21 takes a
+// float quotient: a * rcp(b) is within 0.5 of a / b there (rcp's 1-ulp
+// error times |a / b| < 2^21), so its floor is the quotient or one off, and
+// one correction each way gives the residue exactly; the rest takes the
+// integer division (~25 VALU with quarter-rate multiplies).
+ZHD int32_t fmod_i(int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if ((uint32_t)a < (uint32_t)b) return a;
+    if (b > 0 && a > -(1 << 21) && a < (1 << 21)) {
+        const int32_t q = (int32_t)floorf((float)a * __builtin_amdgcn_rcpf((float)b));
+        int32_t r = a - q * b;
+        r = r < 0 ? r + b : r;
+        return r >= b ? r - b : r;
+    }
+#endif
+    const int32_t r = a % b;
+    return r < 0 ? r + b : r;
+}
 ZHD float lerpf(float a, float b, float t) { return fmaf(b - a, t, a); }       // @mulAdd
 
 struct TexCoords { int32_t i11, i21, i12, i22; float fu, fv; };
