@@ -333,24 +333,34 @@ ZHD bool tri_ray_flat(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, floa
 // ---- textures (stage3.zig:94-121) -----------------------------------------
 ZHD float tex_frac(float v) { return fabsf(v - truncf(v)); }
 ZHD int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
-// @mod(a, b) for b > 0 (texture extents).  On the device |a| < 2^21 (every
-// texel coordinate of a real texture, tiled or not) takes a float quotient:
-// a * rcp(b) is within 0.5 of a / b there (rcp's 1-ulp error times
-// |a / b| < 2^21), so its floor is the quotient or one off, and one
-// correction each way gives the residue exactly; the rest takes the integer
-// division (~25 VALU with quarter-rate multiplies).  (A separate a in [0, b)
-// early return made the primary kernel spill inside its cell walk.)
+// @mod(a, b) for b > 0 (texture extents).  On the device, a in [0, b) --
+// texture coordinates inside the image -- returns a, and |a| < 2^21 takes a
+// float quotient: a * rcp(b) is within 0.5 of a / b there (rcp's 1-ulp
+// error times |a / b| < 2^21), so its floor is the quotient or one off, and
+// one correction each way gives the residue exactly.  The rest takes the
+// integer division (~25 VALU with quarter-rate multiplies) in a call: inline,
+// its registers made the primary kernel spill inside its cell walk, and
+// without the [0, b) return cfg3 lost 3% (r03t/r03u).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __noinline__ int32_t fmod_i_slow(int32_t a, int32_t b) {
+    const int32_t r = a % b;
+    return r < 0 ? r + b : r;
+}
+#endif
 ZHD int32_t fmod_i(int32_t a, int32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    if ((uint32_t)a < (uint32_t)b) return a;
     if (b > 0 && a > -(1 << 21) && a < (1 << 21)) {
         const int32_t q = (int32_t)floorf((float)a * __builtin_amdgcn_rcpf((float)b));
         int32_t r = a - q * b;
         r = r < 0 ? r + b : r;
         return r >= b ? r - b : r;
     }
-#endif
+    return fmod_i_slow(a, b);
+#else
     const int32_t r = a % b;
     return r < 0 ? r + b : r;
+#endif
 }
 ZHD float lerpf(float a, float b, float t) { return fmaf(b - a, t, a); }       // @mulAdd
 
