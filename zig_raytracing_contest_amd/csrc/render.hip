@@ -637,6 +637,15 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
     uint32_t n_seg = 0, dummy = 0;
     uint32_t grp = blockIdx.x & 7u, tried = 0;
+#ifdef ZRT_SWEEP
+    // ZRT_SWEEP builds: per-wave s_memtime cycles of the walk (camera ray +
+    // traceRay), the shading (+ terminal store) and the fetch + append
+    unsigned long long wprof[3] = {0, 0, 0};
+    uint64_t wtick = __builtin_amdgcn_s_memtime();
+#define WF_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); wprof[k] += t_ - wtick; wtick = t_; } while (0)
+#else
+#define WF_STAMP(k) do { } while (0)
+#endif
 
     for (;;) {
         uint32_t base = 0, lim = 0;
@@ -667,8 +676,10 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             }
             float t = kInf, hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
+            WF_STAMP(2);
             if (depth != 0)
                 t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
+            WF_STAMP(0);
             uint32_t item, slot;
             Rng rng;
             path_state<PRIMARY>(w, i, item, depth, slot, rng, mask);
@@ -679,12 +690,19 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             }
             if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
             r_item = item; r_depth = depth; r_slot = slot; r_o = o; r_d = d; r_rng = rng;
+            WF_STAMP(1);
         }
         wf_append(w, cont, below, r_o, r_d, r_item, r_depth, r_slot, r_rng, mask, grp);
+        WF_STAMP(2);
       }
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
+#ifdef ZRT_SWEEP
+    if (PRIMARY && lane == 0)
+        for (int k = 0; k < 3; ++k) atomicAdd(&p.stats[29 + k], wprof[k]);
+#endif
+#undef WF_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -2476,6 +2494,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 "\"pairs\": %llu, \"refill_rounds\": %llu, \"shaded_lanes\": %llu, \"cyc_drain\": %llu, "
                 "\"cyc_atomic\": %llu, \"cyc_setup\": %llu}}\n",
                 hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
+    if (getenv("ZRT_PARK_PROFILE") && !counting)
+        fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
+                hs[29], hs[30], hs[31]);
 #endif
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
