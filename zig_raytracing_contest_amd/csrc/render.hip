@@ -76,6 +76,11 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
+// primary lane walk: exact per-brick cell masks (global) instead of a range
+// load in every cell of an occupied brick
+#ifndef ZRT_PRIM_BMASK
+#define ZRT_PRIM_BMASK 0
+#endif
 constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
 struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -99,6 +104,7 @@ struct TraceParams {
     // their in-brick bits; the 4^3-brick fields for OccX
     PackK pk;
     const uint32_t* cell32;   // 8 u32 per packed cell: begin, end, entry-face masks (see cell32_kernel)
+    const unsigned long long* bmask;   // per 4^3 brick: its 64-bit cell occupancy (null: none kept)
     uint32_t occ_o1, occ_o2, occ_w0, occ_w1, occ_w2, occ_lowm;
     uint32_t ox1, ox2, ow0, ow1, ow2;
     float org[3], llc[3], right[3], up[3];
@@ -167,6 +173,16 @@ __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uin
                        __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
                        __builtin_amdgcn_ubfe(pc, p.occ_shift, p.occ_w0);
     return (occ[b >> 5] >> (b & 31u)) & 1u;
+}
+
+// The in-brick cell index k = x | y << 2 | z << 4 of a packed cell: one
+// 24-bit multiply of the fields' low two bits sums them, shifted into place
+// (pack_layout picks the multiplier and checks every in-brick cell), and the
+// 64-bit shift reads only k[5:0].  (6 VALU; 9 with the fields moved by shifts
+// and masks.)
+__device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
+    const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
+    return (uint32_t)(bm >> (i & 63u)) & 1u;
 }
 
 // Grid constants as wave-uniform registers (see GridK).
@@ -239,19 +255,42 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // every step (r03 ISA)
         uint32_t f0 = p.pk.f0, f1 = p.pk.f1, f2 = p.pk.f2;
         asm("" : "+s"(f0), "+s"(f1), "+s"(f2));
+#if ZRT_PRIM_BMASK
+        // exact occupancy: on entering an occupied brick its 64-bit cell mask
+        // (global, L2-resident) says which cells hold triangles, so only
+        // those load their range (bricks of 4^3 cells: occ_shift 2)
+        auto brick_mask = [&](uint32_t pc) -> unsigned long long {
+            const uint32_t b = __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o2, p.occ_w2), p.occ_nb01) +
+                               __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
+                               __builtin_amdgcn_ubfe(pc, p.occ_shift, p.occ_w0);
+            // (coarser bricks keep no masks: every cell of an occupied one)
+            return ((occ[b >> 5] >> (b & 31u)) & 1u) ? (p.bmask ? p.bmask[b] : ~0ull) : 0ull;
+        };
+        unsigned long long bm = brick_mask(s.pc);
+        for (;;) {
+            if (bm != 0ull && occx_cell(bm, s, p.pk)) {
+                const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
+                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+            }
+#else
         bool occupied = brick_occupied_v(p, occ, s.pc);
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
                 test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
             }
+#endif
             bool crossed, exited;
             float tc;
             PackK pkl = p.pk;
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
             DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
+#if ZRT_PRIM_BMASK
+            if (crossed) bm = brick_mask(s.pc);
+#else
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
+#endif
         }
         return nearest;
     }
@@ -771,15 +810,6 @@ __device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaV& s)
     return __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox2, p.ow2), w.occx_nb01) +
            __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox1, p.ow1), w.occx_nb0) + __builtin_amdgcn_ubfe(s.pc, 2u, p.ow0);
 }
-// The in-brick cell index k = x | y << 2 | z << 4 of a packed cell: one
-// 24-bit multiply of the fields' low two bits sums them, shifted into place
-// (pack_layout picks the multiplier and checks every in-brick cell), and the
-// 64-bit shift reads only k[5:0].  (6 VALU; 9 with the fields moved by shifts
-// and masks.)
-__device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
-    const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
-    return (uint32_t)(bm >> (i & 63u)) & 1u;
-}
 
 // A parked lane's cell range [begin, end) is loaded by LDS-DMA into its
 // wave's slots (begin at rng[lane], end at rng[64 + lane]): the load writes
@@ -791,6 +821,9 @@ __device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, 
 constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_CHUNK
 #define ZRT_PARK_CHUNK 128
+#endif
+#ifndef ZRT_PARK_PREFETCH
+#define ZRT_PARK_PREFETCH 0
 #endif
 // queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
 // 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%)
@@ -938,6 +971,13 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
+#if ZRT_PARK_PREFETCH
+    // the next refill round's rays, loaded at the end of this one: lane L
+    // holds (o, d) of entry pf_cb + L of chunk group pf_grp, so the refill's
+    // first dependent load (the queue record) is off its critical path
+    float pox = 0.0f, poy = 0.0f, poz = 0.0f, pdx = 0.0f, pdy = 0.0f, pdz = 0.0f;
+    uint32_t pf_cb = ~0u, pf_grp = ~0u;
+#endif
     PARK_PROF_DECL
 
     for (;;) {
@@ -975,12 +1015,34 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 const uint32_t take = min((uint32_t)__popcll(idle), ce - cb);
                 const uint32_t rank = (uint32_t)__popcll(idle & below);
+#if ZRT_PARK_PREFETCH
+                // whole wave (full EXEC: a permute reads its source lanes)
+                const bool pf_ok = pf_cb == cb && pf_grp == cgrp;
+                v3 po = mk(0, 0, 0), pd = mk(0, 0, 0);
+                if (pf_ok) {
+                    const int src = (int)(rank << 2);
+                    po = mk(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pox))),
+                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(poy))),
+                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(poz))));
+                    pd = mk(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdx))),
+                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdy))),
+                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdz))));
+                }
+#endif
                 if (st == kIdle && rank < take) {
                     {
                         qi = ent_index<false>(p, cgrp, cb + rank);
-                        const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
-                        o = mk(qa.x, qa.y, qa.z);
-                        d = mk(qb.x, qb.y, qb.z);
+#if ZRT_PARK_PREFETCH
+                        if (pf_ok) {
+                            o = po;
+                            d = pd;
+                        } else
+#endif
+                        {
+                            const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
+                            o = mk(qa.x, qa.y, qa.z);
+                            d = mk(qb.x, qb.y, qb.z);
+                        }
                         {                                          // queued paths have depth >= 1
                             nearest = kInf;
                             hu = hv = 0.0f;
@@ -1007,6 +1069,16 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 cb += take;
                 idle = __ballot(st == kIdle);
             }
+#if ZRT_PARK_PREFETCH
+            pf_cb = cb;
+            pf_grp = cgrp;
+            if (cb + lane < ce) {
+                const uint32_t qj = ent_index<false>(p, cgrp, cb + lane);
+                const float4 qa = w.q_in[3ull * qj], qb = w.q_in[3ull * qj + 1];
+                pox = qa.x; poy = qa.y; poz = qa.z;
+                pdx = qb.x; pdy = qb.y; pdz = qb.z;
+            }
+#endif
             PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
                 if (!more) break;
@@ -1397,6 +1469,7 @@ struct zrt_context {
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
+    unsigned long long* d_bmask = nullptr;   // 64-bit cell mask per 4^3 brick (primary lane walk), if kept
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
     // grow-only work buffers
@@ -1512,7 +1585,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->d_cell32) (void)hipFree(c->d_cell32);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_bmask,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1813,6 +1886,7 @@ __global__ __launch_bounds__(kBlock) void occ_cells_kernel(const uint2* __restri
     }
 }
 
+constexpr bool kKeepBrickMasks = ZRT_PRIM_BMASK != 0;
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     const uint32_t* r = c->grid.resolution;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
@@ -1847,6 +1921,10 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                     }
                 }
         HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
+        if (occx_possible && sh == 2 && kKeepBrickMasks) {
+            HIP_TRY(hipMalloc((void**)&c->d_bmask, nb * 8));
+            HIP_TRY(hipMemcpy(c->d_bmask, mask.data(), nb * 8, hipMemcpyHostToDevice));
+        }
         if (!occx_possible) {
             c->occx_ok = false;
             return context_counters(c);
@@ -1924,6 +2002,10 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         HIP_TRY(hipMemcpyAsync(&run, d_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(le);
+        if (sh == 2 && kKeepBrickMasks) {   // the per-brick masks stay for the primary walk
+            c->d_bmask = tmp.masks;
+            tmp.masks = nullptr;
+        }
         occx_layout(nbw, run, &moff, &words);
         c->occx_ok = occx_usable(nb, run, occx_lds_words(nbw, moff, words) * 4, kOccxBudget);
         c->occx_words = (uint32_t)words;
@@ -2320,6 +2402,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.cells = c->d_cells;
     tp.pk = c->pk;
     tp.cell32 = c->d_cell32;
+    tp.bmask = c->d_bmask;
     {
         const uint32_t sh = c->occ_shift, b[3] = {c->pk.b0, c->pk.b1, c->pk.b2};
         auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
