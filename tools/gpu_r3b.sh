@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 measurement batch: headline bench, sweep-build round profiles
-# (park + primary), then an A/B of the given libraries on cfg3.
+# (park + primary), then an A/B of the given libraries (cfg3, cfg2, cfg5).
 #   LIBS="base: x:tools/bin/x/libzrt.so" bash tools/gpu_r3b.sh TAG
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 tag=${1:-r03b}
@@ -11,11 +11,5 @@ rc=$?; echo "bench rc=$rc"; tail -c 400 $out/bench.json
 [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_parkprof.sh $tag || exit $?
 if [ -n "$LIBS" ]; then
-  log=$out/ab.log; : > $log
-  for rep in 1 2 3; do for spec in $LIBS; do
-    name=${spec%%:*}; L=${spec#*:}
-    ZRT_LIB=$L timeout -k 10 300 python -u tools/kbench.py --config cfg3 --spp 0 --reps 2 --var "" 2>&1 \
-      | grep mrays | sed "s/^/{\"lib\": \"$name\", \"cfg\": \"cfg3\"} /" >> $log || exit 1
-  done; done
-  cat $log
+  bash tools/gpu_ab_full.sh $tag || exit $?
 fi

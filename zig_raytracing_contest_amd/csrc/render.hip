@@ -825,6 +825,10 @@ constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_PREFETCH
 #define ZRT_PARK_PREFETCH 0
 #endif
+// the test round's kept-ref select by an LDS table of byte selects
+#ifndef ZRT_SEL_TABLE
+#define ZRT_SEL_TABLE 0
+#endif
 // queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
 // 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%)
 constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
@@ -888,6 +892,17 @@ __device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t r) {
     return pos;
 }
 
+// select_bit by bytes: the byte holding the r-th set bit from three prefix
+// popcounts, then its position within the byte from an LDS table.
+__device__ __forceinline__ uint32_t select_bit_t(const uint8_t* sel8, uint32_t m, uint32_t r) {
+    const uint32_t c0 = (uint32_t)__popc(m & 0xFFu), c1 = (uint32_t)__popc(m & 0xFFFFu),
+                   c2 = (uint32_t)__popc(m & 0xFFFFFFu);
+    const uint32_t k = (r >= c0 ? 1u : 0u) + (r >= c1 ? 1u : 0u) + (r >= c2 ? 1u : 0u);
+    const uint32_t below = k == 0u ? 0u : (k == 1u ? c0 : (k == 2u ? c1 : c2));
+    const uint32_t byte = __builtin_amdgcn_ubfe(m, 8u * k, 8u);
+    return 8u * k + sel8[byte * 8u + (r - below)];
+}
+
 // Per-wave LDS of the test rounds.
 struct ParkSlot {
     float4 o[64];                    // lane's ray origin; w: nearest entering the round
@@ -938,6 +953,15 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
     uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
+#if ZRT_SEL_TABLE
+    __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
+    for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
+        uint32_t m = i >> 3, r = i & 7u, pos = 0;
+        for (uint32_t k = 0; k < 8; ++k)
+            if ((m >> k) & 1u) { if (r == 0) { pos = k; break; } --r; }
+        s_sel8[i] = (uint8_t)pos;
+    }
+#endif
     // OccX into LDS: (bits, prefix) entries, then the masks
     {
         const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
@@ -1182,7 +1206,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const float4 ro = W.o[owner], rd = W.d[owner];
                 // pair g is the owner's (g - off)-th kept ref
                 const uint32_t kr = g - rng_slot[64 + owner];
+#if ZRT_SEL_TABLE
+                const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit_t(s_sel8, rng_slot[128 + owner], kr) : kr);
+#else
                 const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit(rng_slot[128 + owner], kr) : kr);
+#endif
                 bool cand = false;
                 float t = 0.0f, u = 0.0f, v = 0.0f;
                 if (g < tot) {
@@ -1445,7 +1473,8 @@ constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that ru
 #endif
 constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
-constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256;
+constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256 -
+                                (ZRT_SEL_TABLE ? 2048 : 0);
 
 }  // namespace
 
