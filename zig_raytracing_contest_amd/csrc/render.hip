@@ -76,11 +76,6 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
-// primary lane walk: exact per-brick cell masks (global) instead of a range
-// load in every cell of an occupied brick
-#ifndef ZRT_PRIM_BMASK
-#define ZRT_PRIM_BMASK 0
-#endif
 constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
 struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -104,7 +99,6 @@ struct TraceParams {
     // their in-brick bits; the 4^3-brick fields for OccX
     PackK pk;
     const uint32_t* cell32;   // 8 u32 per packed cell: begin, end, entry-face masks (see cell32_kernel)
-    const unsigned long long* bmask;   // per 4^3 brick: its 64-bit cell occupancy (null: none kept)
     uint32_t occ_o1, occ_o2, occ_w0, occ_w1, occ_w2, occ_lowm;
     uint32_t ox1, ox2, ow0, ow1, ow2;
     float org[3], llc[3], right[3], up[3];
@@ -255,42 +249,19 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // every step (r03 ISA)
         uint32_t f0 = p.pk.f0, f1 = p.pk.f1, f2 = p.pk.f2;
         asm("" : "+s"(f0), "+s"(f1), "+s"(f2));
-#if ZRT_PRIM_BMASK
-        // exact occupancy: on entering an occupied brick its 64-bit cell mask
-        // (global, L2-resident) says which cells hold triangles, so only
-        // those load their range (bricks of 4^3 cells: occ_shift 2)
-        auto brick_mask = [&](uint32_t pc) -> unsigned long long {
-            const uint32_t b = __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o2, p.occ_w2), p.occ_nb01) +
-                               __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
-                               __builtin_amdgcn_ubfe(pc, p.occ_shift, p.occ_w0);
-            // (coarser bricks keep no masks: every cell of an occupied one)
-            return ((occ[b >> 5] >> (b & 31u)) & 1u) ? (p.bmask ? p.bmask[b] : ~0ull) : 0ull;
-        };
-        unsigned long long bm = brick_mask(s.pc);
-        for (;;) {
-            if (bm != 0ull && occx_cell(bm, s, p.pk)) {
-                const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
-                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
-            }
-#else
         bool occupied = brick_occupied_v(p, occ, s.pc);
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
                 test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
             }
-#endif
             bool crossed, exited;
             float tc;
             PackK pkl = p.pk;
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
             DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
-#if ZRT_PRIM_BMASK
-            if (crossed) bm = brick_mask(s.pc);
-#else
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
-#endif
         }
         return nearest;
     }
@@ -558,12 +529,14 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
                        scale(mk(d1.z, d1.w, d2.x), hv));
     const v3 no = add(o, scale(d, t + kFltEps));
     if (!(rng_float(rng) > transparency)) {                 // stage3.zig:207, :214-219
+        // the (e, a) pair goes out before the normal draws, so the ziggurat
+        // (f64, 64-bit RNG) runs without the six colour registers live
+        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
+        w.stk[(2ull * slot + 1) * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
         const float nx = (float)rng_norm64(rng, zx, zf);
         const float ny = (float)rng_norm64(rng, zx, zf);
         const float nz = (float)rng_norm64(rng, zx, zf);
         d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
-        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
-        w.stk[(2ull * slot + 1) * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, 0.0f);
         mask |= 1u << slot;
     }
     o = no;
@@ -822,13 +795,6 @@ constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_CHUNK
 #define ZRT_PARK_CHUNK 128
 #endif
-#ifndef ZRT_PARK_PREFETCH
-#define ZRT_PARK_PREFETCH 0
-#endif
-// the test round's kept-ref select by an LDS table of byte selects
-#ifndef ZRT_SEL_TABLE
-#define ZRT_SEL_TABLE 0
-#endif
 // queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
 // 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%)
 constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
@@ -875,26 +841,12 @@ __device__ __forceinline__ void park_load_cell(const TraceParams& p, uint32_t pc
                  : "memory");
 }
 
-// Position of the r-th (from 0) set bit of m (r < popcount(m)): a binary
-// search over the halves' popcounts.
-__device__ __forceinline__ uint32_t select_bit(uint32_t m, uint32_t r) {
-    uint32_t pos = 0, c;
-    c = (uint32_t)__popc(m & 0xFFFFu);
-    if (r >= c) { r -= c; pos = 16u; }
-    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 8u));
-    if (r >= c) { r -= c; pos += 8u; }
-    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 4u));
-    if (r >= c) { r -= c; pos += 4u; }
-    c = (uint32_t)__popc(__builtin_amdgcn_ubfe(m, pos, 2u));
-    if (r >= c) { r -= c; pos += 2u; }
-    c = __builtin_amdgcn_ubfe(m, pos, 1u);
-    if (r >= c) pos += 1u;
-    return pos;
-}
-
-// select_bit by bytes: the byte holding the r-th set bit from three prefix
-// popcounts, then its position within the byte from an LDS table.
-__device__ __forceinline__ uint32_t select_bit_t(const uint8_t* sel8, uint32_t m, uint32_t r) {
+// Position of the r-th (from 0) set bit of m (r < popcount(m)): the byte
+// holding it from three prefix popcounts, then its position within the byte
+// from an LDS table (sel8[byte * 8 + rank]).  ~20 VALU + one LDS read against
+// ~35 dependent VALU for a binary search over the halves' popcounts (r03v:
+// cfg3 +0.7%, cfg5 +0.6%).
+__device__ __forceinline__ uint32_t select_bit(const uint8_t* sel8, uint32_t m, uint32_t r) {
     const uint32_t c0 = (uint32_t)__popc(m & 0xFFu), c1 = (uint32_t)__popc(m & 0xFFFFu),
                    c2 = (uint32_t)__popc(m & 0xFFFFFFu);
     const uint32_t k = (r >= c0 ? 1u : 0u) + (r >= c1 ? 1u : 0u) + (r >= c2 ? 1u : 0u);
@@ -953,7 +905,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
     uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
-#if ZRT_SEL_TABLE
     __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
     for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
         uint32_t m = i >> 3, r = i & 7u, pos = 0;
@@ -961,7 +912,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             if ((m >> k) & 1u) { if (r == 0) { pos = k; break; } --r; }
         s_sel8[i] = (uint8_t)pos;
     }
-#endif
     // OccX into LDS: (bits, prefix) entries, then the masks
     {
         const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
@@ -995,13 +945,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
-#if ZRT_PARK_PREFETCH
-    // the next refill round's rays, loaded at the end of this one: lane L
-    // holds (o, d) of entry pf_cb + L of chunk group pf_grp, so the refill's
-    // first dependent load (the queue record) is off its critical path
-    float pox = 0.0f, poy = 0.0f, poz = 0.0f, pdx = 0.0f, pdy = 0.0f, pdz = 0.0f;
-    uint32_t pf_cb = ~0u, pf_grp = ~0u;
-#endif
     PARK_PROF_DECL
 
     for (;;) {
@@ -1039,29 +982,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 const uint32_t take = min((uint32_t)__popcll(idle), ce - cb);
                 const uint32_t rank = (uint32_t)__popcll(idle & below);
-#if ZRT_PARK_PREFETCH
-                // whole wave (full EXEC: a permute reads its source lanes)
-                const bool pf_ok = pf_cb == cb && pf_grp == cgrp;
-                v3 po = mk(0, 0, 0), pd = mk(0, 0, 0);
-                if (pf_ok) {
-                    const int src = (int)(rank << 2);
-                    po = mk(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pox))),
-                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(poy))),
-                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(poz))));
-                    pd = mk(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdx))),
-                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdy))),
-                            __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(pdz))));
-                }
-#endif
                 if (st == kIdle && rank < take) {
                     {
                         qi = ent_index<false>(p, cgrp, cb + rank);
-#if ZRT_PARK_PREFETCH
-                        if (pf_ok) {
-                            o = po;
-                            d = pd;
-                        } else
-#endif
                         {
                             const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
                             o = mk(qa.x, qa.y, qa.z);
@@ -1093,16 +1016,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 cb += take;
                 idle = __ballot(st == kIdle);
             }
-#if ZRT_PARK_PREFETCH
-            pf_cb = cb;
-            pf_grp = cgrp;
-            if (cb + lane < ce) {
-                const uint32_t qj = ent_index<false>(p, cgrp, cb + lane);
-                const float4 qa = w.q_in[3ull * qj], qb = w.q_in[3ull * qj + 1];
-                pox = qa.x; poy = qa.y; poz = qa.z;
-                pdx = qb.x; pdy = qb.y; pdz = qb.z;
-            }
-#endif
             PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
                 if (!more) break;
@@ -1206,11 +1119,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const float4 ro = W.o[owner], rd = W.d[owner];
                 // pair g is the owner's (g - off)-th kept ref
                 const uint32_t kr = g - rng_slot[64 + owner];
-#if ZRT_SEL_TABLE
-                const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit_t(s_sel8, rng_slot[128 + owner], kr) : kr);
-#else
-                const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit(rng_slot[128 + owner], kr) : kr);
-#endif
+                const uint32_t j = rng_slot[owner] + (kr < 32u ? select_bit(s_sel8, rng_slot[128 + owner], kr) : kr);
                 bool cand = false;
                 float t = 0.0f, u = 0.0f, v = 0.0f;
                 if (g < tot) {
@@ -1474,7 +1383,7 @@ constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that ru
 constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256 -
-                                (ZRT_SEL_TABLE ? 2048 : 0);
+                                256 * 8;   // the select table
 
 }  // namespace
 
@@ -1498,7 +1407,6 @@ struct zrt_context {
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
-    unsigned long long* d_bmask = nullptr;   // 64-bit cell mask per 4^3 brick (primary lane walk), if kept
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
     // grow-only work buffers
@@ -1614,7 +1522,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->d_cell32) (void)hipFree(c->d_cell32);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_bmask,
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1915,7 +1823,6 @@ __global__ __launch_bounds__(kBlock) void occ_cells_kernel(const uint2* __restri
     }
 }
 
-constexpr bool kKeepBrickMasks = ZRT_PRIM_BMASK != 0;
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     const uint32_t* r = c->grid.resolution;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
@@ -1950,10 +1857,6 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                     }
                 }
         HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
-        if (occx_possible && sh == 2 && kKeepBrickMasks) {
-            HIP_TRY(hipMalloc((void**)&c->d_bmask, nb * 8));
-            HIP_TRY(hipMemcpy(c->d_bmask, mask.data(), nb * 8, hipMemcpyHostToDevice));
-        }
         if (!occx_possible) {
             c->occx_ok = false;
             return context_counters(c);
@@ -2031,10 +1934,6 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         HIP_TRY(hipMemcpyAsync(&run, d_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(le);
-        if (sh == 2 && kKeepBrickMasks) {   // the per-brick masks stay for the primary walk
-            c->d_bmask = tmp.masks;
-            tmp.masks = nullptr;
-        }
         occx_layout(nbw, run, &moff, &words);
         c->occx_ok = occx_usable(nb, run, occx_lds_words(nbw, moff, words) * 4, kOccxBudget);
         c->occx_words = (uint32_t)words;
@@ -2431,7 +2330,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.cells = c->d_cells;
     tp.pk = c->pk;
     tp.cell32 = c->d_cell32;
-    tp.bmask = c->d_bmask;
     {
         const uint32_t sh = c->occ_shift, b[3] = {c->pk.b0, c->pk.b1, c->pk.b2};
         auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
