@@ -196,6 +196,7 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
                                       f"{conf['num_samples']} max_bounce {conf['max_bounce']}: "
                                       "'Done in' (main.zig:78 -> :142), min of "
                                       f"{reps} runs", "done_in_ms": [round(x, 2) for x in done],
+                              "done_in_median_ms": round(sorted(done)[len(done) // 2], 2),
                               "process_ms": [round(x, 2) for x in wall],
                               "cli_rays": rays.group(0) if rays else None,
                               "stages_ms_last_run": stages}}
