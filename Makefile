@@ -44,8 +44,10 @@ $(PROBE): tools/dpp_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
-# Tuning build (tools only, never loaded by tests or bench): the park-kernel
-# schedule read from ZRT_PARK_T / ZRT_PARK_R; used through ZRT_LIB=<path>.
+# Tuning build: the park-kernel schedule read from ZRT_PARK_T / ZRT_PARK_R,
+# ZRT_SETS, and the s_memtime round profiles (ZRT_PARK_PROFILE); used through
+# ZRT_LIB=<path> by tools/ and by the schedule-extreme and pass-set parity
+# tests (tests/test_gpu_parity.py), never by bench.py or the product path.
 sweep: $(SWEEP_LIB)
 $(SWEEP_LIB): $(SRC)/render.hip $(HDRS) $(filter-out $(OBJ)/render.o,$(HIP_OBJS)) $(HOST_OBJS)
 	@mkdir -p tools/bin/sweep
