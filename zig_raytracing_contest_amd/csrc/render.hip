@@ -1323,13 +1323,20 @@ using WfFn = void (*)(const WfParams);
 #endif
 constexpr int kWfMinWaves = ZRT_WF_MINW;
 constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
-// wf_park_kernel schedule: a test round once 12 lanes are parked, a shade +
+// wf_park_kernel schedule: a test round once 14 lanes are parked, a shade +
 // refill round once 16 lanes are finished (cfg3 64 spp sweep, r02d: T 4-16 x
 // R 8/16/32; T 12 R 16 3110 Mrays/s, T 8-16 R 16 within 1.3%, R 8 -15%,
-// R 32 -13%; cfg5 T 16 R 16 2075, T 8 2055).  ZRT_SWEEP builds read
-// ZRT_PARK_T / ZRT_PARK_R.
-constexpr uint32_t kParkTestMin = 12;
-constexpr uint32_t kParkRefillMin = 16;
+// R 32 -13%; cfg5 T 16 R 16 2075, T 8 2055; full spp after the lane-mask
+// trip, r03z: T 14 vs 12 cfg3 +0.3%, cfg2 +0.6%, cfg5 +0.5%; T 10 / 16,
+// R 12 / 20 no better).  ZRT_SWEEP builds read ZRT_PARK_T / ZRT_PARK_R.
+#ifndef ZRT_PARK_T
+#define ZRT_PARK_T 14
+#endif
+#ifndef ZRT_PARK_R
+#define ZRT_PARK_R 16
+#endif
+constexpr uint32_t kParkTestMin = ZRT_PARK_T;
+constexpr uint32_t kParkRefillMin = ZRT_PARK_R;
 // packed walk state when every axis has at most kPackMaxRes cells
 const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true, true>;
 const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false, true>;
