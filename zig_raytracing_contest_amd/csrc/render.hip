@@ -793,10 +793,12 @@ __device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaV& s)
 // wave's own vmcnt, so the test round drains vmcnt(0) before reading them.
 constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_CHUNK
-#define ZRT_PARK_CHUNK 128
+#define ZRT_PARK_CHUNK 256
 #endif
 // queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
-// 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%)
+// 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%;
+// r03za, on the round-3 kernels: 256 vs 128 cfg3 +0.5%, cfg5 +0.4%, cfg2
+// -0.5%; 64 -0.7 / -1.0 / -0.5%)
 constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
