@@ -50,7 +50,12 @@ constexpr float kFltEps = 1.1920928955078125e-07f;   // std.math.floatEps(f32)
 constexpr int kBlock = 256;                          // resolve / probes / helpers
 constexpr int kTraceBlock = 512;                     // launch bound of wf_kernel / trace_kernel
 constexpr int kTraceThreads = 256;                   // threads per wf_kernel / trace_kernel block
-constexpr int kTriBatch = 2;                         // triangle loads in flight per lane
+// (r03ze, full spp: 1 -1.3 / -0.6 / -1.5%, 3 -0.6 / -0.2 / -0.6% on cfg3 /
+// cfg2 / cfg5; 3 spills inside the primary's cell walk)
+#ifndef ZRT_TRI_BATCH
+#define ZRT_TRI_BATCH 2
+#endif
+constexpr int kTriBatch = ZRT_TRI_BATCH;             // triangle loads in flight per lane
 constexpr int kParkBlock = 1024;                     // wf_park_kernel: one workgroup per CU
 #ifndef ZRT_SHADE_N
 #define ZRT_SHADE_N 2
