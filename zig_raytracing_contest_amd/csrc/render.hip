@@ -800,10 +800,6 @@ constexpr int kParkWaves = kParkBlock / 64;
 #ifndef ZRT_PARK_CHUNK
 #define ZRT_PARK_CHUNK 256
 #endif
-// test rounds prefetch their parked cells' triangle lines (LDS-DMA)
-#ifndef ZRT_TEST_PREFETCH
-#define ZRT_TEST_PREFETCH 0
-#endif
 // queue entries per work atomic of a park wave (r02d0, two pass sets: 128 vs
 // 64 cfg3 +0.8%, cfg2 +1.1%, cfg5 +0.3%; 32 -2%; 256 +1.0 / -0.1 / +0.5%;
 // r03za, on the round-3 kernels: 256 vs 128 cfg3 +0.5%, cfg5 +0.4%, cfg2
@@ -916,10 +912,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
     uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
-#if ZRT_TEST_PREFETCH
-    __shared__ uint32_t s_pf[kParkWaves * 64];              // dummy destination of the triangle prefetches
-    uint32_t* const pf_slot = s_pf + 64u * (threadIdx.x >> 6);
-#endif
     __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
     for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
         uint32_t m = i >> 3, r = i & 7u, pos = 0;
@@ -1108,27 +1100,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane], cnt = re - rb;
             const uint32_t keep = cnt < 32u ? rng_slot[128 + lane] & ((1u << cnt) - 1u) : rng_slot[128 + lane];
             const uint32_t n = ready ? (cnt <= 32u ? (uint32_t)__popc(keep) : cnt) : 0u;
-#if ZRT_TEST_PREFETCH
-            // pull the parked cells' triangles toward L1/L2 while the pairs
-            // are laid out: one 4-byte LDS-DMA per 128-byte line of each
-            // parked range (at most 8 lines), landing in a dummy slot
-            {
-                const uint64_t l0 = ((uint64_t)rb * (kTriFloats * 4u)) >> 7;
-                const uint64_t l1 = ((uint64_t)re * (kTriFloats * 4u) + 127u) >> 7;
-                const uint32_t nl = n != 0u ? (uint32_t)min<uint64_t>(l1 - l0, 8u) : 0u;
-                const char* const base = reinterpret_cast<const char*>(p.tri_pos);
-                const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)pf_slot);
-                for (uint32_t i = 0; __ballot(i < nl) != 0ull; ++i)
-                    if (i < nl) {
-                        const char* a = base + ((l0 + i) << 7);
-                        asm volatile("s_mov_b32 m0, %1\n\t"
-                                     "global_load_lds_dword %0, off"
-                                     :
-                                     : "v"(a), "s"(m0)
-                                     : "memory");
-                    }
-            }
-#endif
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
             PARK_COUNT(5, 1);
@@ -1426,8 +1397,7 @@ constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that ru
 constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256 -
-                                256 * 8 -  // the select table
-                                (ZRT_TEST_PREFETCH ? kParkWaves * 64 * 4 : 0);
+                                256 * 8;   // the select table
 
 }  // namespace
 
