@@ -422,4 +422,33 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
         (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
     } while (0)
 
+// Select of the park kernel's pair refill (render.hip): position of the r-th
+// (from 0) set bit of m, r < popcount(m).  The byte holding it comes from
+// three prefix popcounts, its position within the byte from a 2 KB LDS table
+// (sel8[byte * 8 + rank], filled with SEL8_ENTRY).  ~20 VALU + one LDS read
+// against ~35 dependent VALU for a binary search over the halves' popcounts
+// (r03v: cfg3 +0.7%, cfg5 +0.6%).  tests/cpp/select_check.cpp checks it
+// against a bit loop on the host.
+// A macro rather than a function: as a call the table fill reshuffles the park
+// kernel's register allocation (same instructions, other registers).
+#define SEL8_ENTRY(I, POS)                                                         \
+    uint32_t POS = 0;                                                              \
+    {                                                                              \
+        uint32_t m_ = (I) >> 3, r_ = (I) & 7u;                                     \
+        for (uint32_t k_ = 0; k_ < 8; ++k_)                                        \
+            if ((m_ >> k_) & 1u) { if (r_ == 0) { POS = k_; break; } --r_; }       \
+    }
+ZHD uint32_t select_bit(const uint8_t* sel8, uint32_t m, uint32_t r) {
+    const uint32_t c0 = (uint32_t)__builtin_popcount(m & 0xFFu), c1 = (uint32_t)__builtin_popcount(m & 0xFFFFu),
+                   c2 = (uint32_t)__builtin_popcount(m & 0xFFFFFFu);
+    const uint32_t k = (r >= c0 ? 1u : 0u) + (r >= c1 ? 1u : 0u) + (r >= c2 ? 1u : 0u);
+    const uint32_t below = k == 0u ? 0u : (k == 1u ? c0 : (k == 2u ? c1 : c2));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t byte = __builtin_amdgcn_ubfe(m, 8u * k, 8u);
+#else
+    const uint32_t byte = (m >> (8u * k)) & 0xFFu;
+#endif
+    return 8u * k + sel8[byte * 8u + (r - below)];
+}
+
 }  // namespace zrt

@@ -848,20 +848,6 @@ __device__ __forceinline__ void park_load_cell(const TraceParams& p, uint32_t pc
                  : "memory");
 }
 
-// Position of the r-th (from 0) set bit of m (r < popcount(m)): the byte
-// holding it from three prefix popcounts, then its position within the byte
-// from an LDS table (sel8[byte * 8 + rank]).  ~20 VALU + one LDS read against
-// ~35 dependent VALU for a binary search over the halves' popcounts (r03v:
-// cfg3 +0.7%, cfg5 +0.6%).
-__device__ __forceinline__ uint32_t select_bit(const uint8_t* sel8, uint32_t m, uint32_t r) {
-    const uint32_t c0 = (uint32_t)__popc(m & 0xFFu), c1 = (uint32_t)__popc(m & 0xFFFFu),
-                   c2 = (uint32_t)__popc(m & 0xFFFFFFu);
-    const uint32_t k = (r >= c0 ? 1u : 0u) + (r >= c1 ? 1u : 0u) + (r >= c2 ? 1u : 0u);
-    const uint32_t below = k == 0u ? 0u : (k == 1u ? c0 : (k == 2u ? c1 : c2));
-    const uint32_t byte = __builtin_amdgcn_ubfe(m, 8u * k, 8u);
-    return 8u * k + sel8[byte * 8u + (r - below)];
-}
-
 // Per-wave LDS of the test rounds.
 struct ParkSlot {
     float4 o[64];                    // lane's ray origin; w: nearest entering the round
@@ -914,9 +900,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
     __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
     for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
-        uint32_t m = i >> 3, r = i & 7u, pos = 0;
-        for (uint32_t k = 0; k < 8; ++k)
-            if ((m >> k) & 1u) { if (r == 0) { pos = k; break; } --r; }
+        SEL8_ENTRY(i, pos);
         s_sel8[i] = (uint8_t)pos;
     }
     // OccX into LDS: (bits, prefix) entries, then the masks
