@@ -23,6 +23,12 @@ Beside the timed loop (rank 0, N = 1, after it):
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-wall-clock]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+         or plain `python bench.py --gpus N`: with no WORLD_SIZE in the
+         environment the process (which has made no HIP call) starts the N
+         ranks itself through torch.distributed.run, relays rank 0's line and
+         exits with the launcher's status.  A WORLD_SIZE that disagrees with
+         --gpus is an error (exit 2): the frame must not silently run on
+         fewer GPUs than asked (the reference's partition, stage3.zig:228-229).
 
 Rank 0 prints ONE JSON line, with the sha1 of the whole frame (img_sha1: the
 same for any N, asserted equal to the untimed counting frame's).  Image tiles
@@ -107,6 +113,13 @@ def cgroup_cpu_quota():
         return None
 
 
+def effective_cpus(threads):
+    """CPUs the threads can really run on at once: min(affinity mask, cgroup
+    cpu.max quota rounded up).  256 threads under a 16-CPU quota share 16."""
+    q = cgroup_cpu_quota()
+    return max(1, min(threads, int(-(-q // 1)))) if q else threads
+
+
 def cpu_baseline(soup, cfg, target_s):
     """Oracle in REF mode (the reference's Xoshiro-per-thread, contiguous
     blocks, recursion; gcc -O3, no fast-math) on a bounded, evenly spread
@@ -143,12 +156,15 @@ def cpu_baseline(soup, cfg, target_s):
                                           f"{int(ctr[0])} segments in {dt:.1f}s")
 
     v, sample = measure(threads, target_s)
-    out = {"value": round(v, 3), "unit": "Mrays/s", "cores": threads, "cores_available": threads,
-           "cgroup_cpu_quota": cgroup_cpu_quota(), "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-           "kind": "port",
+    eff = effective_cpus(threads)
+    out = {"value": round(v, 3), "unit": "Mrays/s", "cores": eff, "effective_cpus": eff,
+           "threads": threads, "value_per_effective_cpu": round(v / eff, 4),
+           "cgroup_cpu_quota": cgroup_cpu_quota(), "affinity_cpus": threads, "nproc": os.cpu_count(),
+           "cpu_model": cpu_model(), "kind": "port",
            "sample": f"{sample}; oracle REF mode (Xoshiro256++ per thread, contiguous blocks, "
                      f"recursion), gcc -O3, {threads} threads = every CPU of the affinity mask "
-                     "(num_threads null -> getCpuCount, main.zig:90)"}
+                     "(num_threads null -> getCpuCount, main.zig:90), sharing "
+                     f"{eff} effective CPUs (min of the affinity mask and the cgroup quota)"}
     if capped < threads:
         vc, sc = measure(capped, target_s / 2)
         out["omp_capped"] = {"value": round(vc, 3), "cores": capped, "sample": sc,
@@ -235,7 +251,10 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
                         "grid build + bake (oracle, single-threaded as stage2.zig), render (oracle REF mode, "
                         f"{threads} threads), PNG save (zlib); Python process already running",
                 "stages_ms": {k: round(v * 1e3, 2) for k, v in t.items()},
-                "segments": int(ctr[0]), "cores": threads}
+                "segments": int(ctr[0]), "threads": threads, "cores": effective_cpus(threads),
+                "effective_cpus": effective_cpus(threads),
+                "render_mrays_per_effective_cpu": round(int(ctr[0]) / t["render"] / 1e6
+                                                        / effective_cpus(threads), 4)}
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -263,9 +282,59 @@ def roofline_profile_for(config, one_set_kernel="wf_park_kernel"):
 PEAK_VALU_GLANE = 256 * 4 * 32 * 2.4
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command that starts this bench on n ranks
+    of one node (the driver's own N > 1 form), with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(gpus, env):
+    """(world size to run at here, or None: spawn the ranks first).  Raises
+    SystemExit(2) when the launcher's WORLD_SIZE disagrees with --gpus."""
+    if "WORLD_SIZE" not in env:
+        return None if gpus > 1 else 1
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (the launcher started a different number "
+              "of ranks)", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    return world
+
+
+def spawn_ranks(n, argv):
+    """No launcher around us and --gpus n > 1: start the n ranks (this
+    process has made no HIP or torch-device call), relay rank 0's JSON line on
+    stdout (everything else to stderr), return the launcher's exit status
+    (non-zero when any rank failed)."""
+    cmd = launcher_cmd(n, argv, free_port())
+    print("bench.py: starting %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in p.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = world_check(a.gpus, os.environ)
+    if world is None:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = torch = None

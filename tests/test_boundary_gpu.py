@@ -158,3 +158,11 @@ def test_bench_entry_two_ranks_gloo_matches_one():
     assert j1["n_gpus"] == 1 and j2["n_gpus"] == 2
     assert j1["img_sha1"] and j2["img_sha1"] == j1["img_sha1"]
     assert j2["config"]["segments_per_step"] == j1["config"]["segments_per_step"]
+    # the driver's plain form, no launcher: bench.py starts its own 2 ranks
+    env.pop("WORLD_SIZE", None)
+    own = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo"]
+                         + common, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert own.returncode == 0, own.stderr[-3000:]
+    j3 = _bench_json(own.stdout)
+    assert j3["n_gpus"] == 2 and j3["img_sha1"] == j1["img_sha1"]
+    assert j3["config"]["parallelism"] == "tiles2"

@@ -3,8 +3,8 @@
 Every BASELINE config the bench and the config log quote (cfg2, cfg3, cfg5,
 and cfg4 on one GPU) is rendered at FULL size with the product kernels and
 the product schedule -- the pass split of the 144 GiB budget, two pass sets on
-two HIP streams with the lead, 128-entry park chunks over hundreds of millions
-of queue entries -- and a pixel subset of the frame is compared against the
+two HIP streams with the lead, kParkChunk-entry park chunks (render.hip) over
+hundreds of millions of queue entries, pixel-major items -- and a pixel subset of the frame is compared against the
 oracle's render_pixels (oracle/zrt_oracle.c, the reference's renderWorker
 restated, stage3.zig:222-245) with the same counter RNG: RGB8 AND linear
 radiance bit-equal.  The subset is every 499th pixel plus every pixel of two

@@ -2,6 +2,7 @@
 # Counter availability + LDS/issue counters of the park kernel (one-stream bench, cfg3)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 out=gpurun_out/${1:-lds}
+shift   # the rest are counter groups, one rocprofv3 pass each
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > $out/avail.txt 2>&1 || true

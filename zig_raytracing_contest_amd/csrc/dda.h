@@ -211,12 +211,33 @@ ZHD bool pack_fields(uint32_t b0, uint32_t b1, uint32_t b2, PackK& k) {
     k.kshr = sh;
     k.kmul = (1u << sh) + (1u << (sh + 2u - k.o1)) + (1u << (sh + 4u - k.o2));
     if (k.kmul >= (1u << 24)) return false;                    // a 24-bit multiply operand
+    if (k.o2 + 2u > 24u) return false;                         // pc & low2 must fit 24 bits too
     for (uint32_t c = 0; c < 64; ++c) {
         const uint32_t t = (c & 3u) | (((c >> 2) & 3u) << k.o1) | ((c >> 4) << k.o2);
-        if ((((t * k.kmul) >> k.kshr) & 63u) != c) return false;
+        // exactly the kernels' __umul24 (24-bit operands, low 32 bits of the product)
+        if (((((t & 0xFFFFFFu) * (k.kmul & 0xFFFFFFu)) >> k.kshr) & 63u) != c) return false;
     }
     return true;
 }
+// Division of a pass item (< 2^31) by the pass's samples per pixel S, as one
+// 32x32->64 multiply and a shift (Granlund-Montgomery with N = 31:
+// m = ceil(2^(31+l) / S), l = ceil(log2 S), so 2^(31+l) <= m S < 2^(31+l) + 2^l
+// and floor(n m / 2^(31+l)) = floor(n / S) for every n < 2^31; m < 2^32 for
+// S < 2^31).  Items are pixel-major (item = q S + s), so q = item / S is the
+// pixel and item - q S the sample (tests/cpp/div_check.cpp: every S < 2^16).
+struct DivS {
+    uint32_t m, sh;
+};
+ZHD DivS div_magic(uint32_t S) {
+    uint32_t l = 0;
+    while (l < 31 && (1ull << l) < S) ++l;
+    DivS r;
+    r.sh = 31u + l;
+    r.m = (uint32_t)(((1ull << r.sh) + S - 1) / S);
+    return r;
+}
+ZHD uint32_t div_by(uint32_t n, const DivS& d) { return (uint32_t)(((uint64_t)n * d.m) >> d.sh); }
+
 // The layout for a grid; false if it does not pack (an axis above 1024
 // cells).  Fields as narrow as the resolution allows (then the word is the
 // linear index on power-of-two grids), widened where close fields would make

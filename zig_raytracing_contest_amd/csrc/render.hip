@@ -7,9 +7,10 @@
 //
 // Organisation (MI355X-first, not the reference's thread blocks):
 //   * a work item is ONE path sample (pixel, sample); items are numbered
-//     sample-major over this rank's packed pixel list (64x64 tiles walked in
-//     8x8 blocks, so one wave64 = one 8x8 pixel block of one sample index:
-//     coherent primary rays);
+//     pixel-major over this rank's packed pixel list (64x64 tiles walked in
+//     8x8 blocks), item = pixel * S + sample of the pass, so one wave64 of
+//     the primary launch = 64 samples of one pixel (coherent primary rays)
+//     and its records are contiguous;
 //   * bounce k of every path of a pass is one launch over a compacted queue
 //     of the paths still alive (wavefront organisation); each lane traces one
 //     Scene.traceRay segment and shades it (traceRayRecursive's body);
@@ -111,7 +112,9 @@ struct TraceParams {
     const uint32_t* pixlist;
     uint32_t P;               // pixels of this rank
     uint32_t s0;              // first sample index of this pass
-    uint32_t total;           // items in this pass
+    uint32_t total;           // items in this pass: S * P, pixel-major (item = q * S + s)
+    uint32_t S;               // samples of every pixel in this pass
+    DivS sdiv;                // item / S by multiply and shift (div_magic)
     uint32_t max_bounce;
     uint64_t seed;
     float4* out;              // counting build: sample radiance per item
@@ -331,10 +334,12 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 // renderWorker: camera.getRay(x + U, y + U) (stage3.zig:238, :27-35) for
-// pass item `item` (= s_local * P + packed pixel); leaves rng after the jitter.
+// pass item `item` (= packed pixel * S + s_local: pixel-major, so one
+// pixel's samples are consecutive items and a wave's records are
+// contiguous); leaves rng after the jitter.
 __device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, Rng& rng, v3& o, v3& d) {
-    const uint32_t s_local = item / p.P;
-    const uint32_t q = item - s_local * p.P;
+    const uint32_t q = div_by(item, p.sdiv);
+    const uint32_t s_local = item - q * p.S;
     const uint32_t pixel = p.pixlist[q];
     const uint32_t py = pixel / p.w;
     const uint32_t px = pixel - py * p.w;
@@ -349,8 +354,9 @@ __device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, 
 
 // The RNG state camera_ray leaves (after the jitter draws), without the ray.
 __device__ __forceinline__ Rng camera_rng(const TraceParams& p, uint32_t item) {
-    const uint32_t s_local = item / p.P;
-    const uint32_t pixel = p.pixlist[item - s_local * p.P];
+    const uint32_t q = div_by(item, p.sdiv);
+    const uint32_t s_local = item - q * p.S;
+    const uint32_t pixel = p.pixlist[q];
     Rng rng;
     rng.s = path_key(p.seed, pixel, p.s0 + s_local);
     (void)rng_float(rng);
@@ -468,6 +474,7 @@ __global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams
 // stores its terminal radiance (env / 0) and the mask of bounce slots that
 // scattered.  The per-bounce (emissive, albedo) pairs go to HBM in
 // [slot][item] planes and wf_resolve_kernel folds them back to front.
+// Items are pixel-major (item = packed pixel * S + sample of the pass).
 //
 // A queue record is 48 B: (o.xyz, item) (d.xyz, depth | slot << 16)
 // (rng lo, rng hi, mask, 0).
@@ -482,7 +489,8 @@ struct WfParams {
     TraceParams t;
     const float4* q_in;
     float4* q_out;
-    float4* stk;              // plane 2*slot: float4 (e, a.x) [item]; plane 2*slot+1: float2 (a.y, a.z) [item]
+    float4* stk4;             // bounce planes, slot-major: float4 (e, a.x) at [slot * T + item]
+    float2* stk2;             //   and float2 (a.y, a.z) at [slot * T + item] (24 B per pair)
     float4* term;             // [item]: terminal L.xyz, scatter mask bits
     uint32_t T;               // items in this pass
     uint32_t* fetch8;         // work counter per group of this launch
@@ -538,8 +546,8 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
         // (f64, 64-bit RNG) runs without the six colour registers live; 24 B
         // per pair instead of two float4 (r03zk: cfg3 +0.5%, cfg2 +1.6%,
         // cfg5 +1.3%: this write and wf_resolve_kernel's read are HBM-bound)
-        w.stk[(2ull * slot) * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, albedo.x);
-        reinterpret_cast<float2*>(w.stk + (2ull * slot + 1) * w.T)[item] = make_float2(albedo.y, albedo.z);
+        w.stk4[(uint64_t)slot * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, albedo.x);
+        w.stk2[(uint64_t)slot * w.T + item] = make_float2(albedo.y, albedo.z);
         const float nx = (float)rng_norm64(rng, zx, zf);
         const float ny = (float)rng_norm64(rng, zx, zf);
         const float nz = (float)rng_norm64(rng, zx, zf);
@@ -567,7 +575,7 @@ __device__ __forceinline__ void q_store(const WfParams& w, uint32_t pos, v3 o, v
 __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d, uint32_t item,
                                           uint32_t depth, uint32_t slot, const Rng& rng, uint32_t mask,
                                           uint32_t reg) {
-    const uint32_t S = w.t.total / max(w.t.P, 1u);
+    const uint32_t S = w.t.S;
     uint64_t pend = __ballot(cont);
     while (pend) {
         const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
@@ -591,7 +599,7 @@ template <bool PRIMARY>
 __device__ __forceinline__ bool wf_fetch(const WfParams& w, uint32_t want, uint32_t& grp, uint32_t& tried,
                                          uint32_t& base, uint32_t& lim) {
     const TraceParams& p = w.t;
-    const uint32_t S = p.total / max(p.P, 1u);
+    const uint32_t S = p.S;
     for (;;) {
         const uint32_t q0 = xcd_q0(p.P, grp);
         const uint32_t pg = xcd_q0(p.P, grp + 1u) - q0;
@@ -610,15 +618,15 @@ __device__ __forceinline__ bool wf_fetch(const WfParams& w, uint32_t want, uint3
 // stay within one pixel's footprint walk the same cells and test the same
 // triangles side by side.  Against 64 pixels of one sample (8x8 blocks,
 // sample-major) the primary launch took 17.0 vs 22.4-23.2 ms at cfg3 64 spp
-// (r02at: cfg3 +6.3%, cfg5 +3.6%, cfg2 +0.5%).  The item number (sample *
-// P + pixel, what term / stk / resolve index) is unchanged: same image.
+// (r02at: cfg3 +6.3%, cfg5 +3.6%, cfg2 +0.5%).  Since r04 the item number
+// (what term / the bounce planes / the resolve index) is pixel-major too,
+// item = S * pixel + sample = S * q0 + j: a wave's terminal and bounce-pair
+// stores are contiguous (sample-major, its 64 lanes stored 64 lines P items
+// apart: 126 B of DRAM writes per primary item for <= 72 B of records, r03zm).
+// Bounce launches: entry j of region g is queue index S * q0 + j.
 template <bool PRIMARY>
 __device__ __forceinline__ uint32_t ent_index(const TraceParams& p, uint32_t grp, uint32_t j) {
-    const uint32_t S = p.total / max(p.P, 1u);
-    const uint32_t q0 = xcd_q0(p.P, grp);
-    const uint32_t pg = xcd_q0(p.P, grp + 1u) - q0;
-    (void)pg;
-    return PRIMARY ? (j % S) * p.P + q0 + j / S : S * q0 + j;
+    return p.S * xcd_q0(p.P, grp) + j;
 }
 
 // The path state of queue entry / primary item `i` that shading needs.
@@ -1240,30 +1248,54 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
 
 // Fold + ordered sample sum + toRGB for wavefront mode (stage3.zig:219,
 // :236-242): per sample, L = terminal radiance, then e + a*L for every slot
-// that scattered, from the last bounce back to the first.
+// that scattered, from the last bounce back to the first.  Items are
+// pixel-major, so a block takes kResPix pixels and folds their samples
+// kResSmp at a time with consecutive lanes on consecutive items (16 lanes
+// read one pixel's 16 records: 256-byte runs), parks the radiances in LDS,
+// and one thread per pixel then adds them in sample order (renderWorker's
+// `pixel = pixel.add(...)` chain, unchanged: the same f32 sum).
+constexpr uint32_t kResPix = 64, kResSmp = 16, kResRow = kResSmp * 3 + 1;   // +1: no LDS bank conflict
 __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(const float4* __restrict__ term,
-                                                            const float4* __restrict__ stk, uint32_t T,
+                                                            const float4* __restrict__ stk4,
+                                                            const float2* __restrict__ stk2, uint32_t T,
                                                             uint32_t P, uint32_t S, uint32_t max_bounce,
                                                             float4* acc, int first, int last,
                                                             float inv_spp, uint8_t* rgb, float* lin) {
-    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
-    if (q >= P) return;
+    __shared__ float s_l[kResPix * kResRow];
+    const uint32_t q0 = blockIdx.x * kResPix;
+    const uint32_t np = min(kResPix, P - q0);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = q0 + tid;
     v3 px = mk(0, 0, 0);
-    if (!first) { const float4 a = acc[q]; px = mk(a.x, a.y, a.z); }
-    for (uint32_t s = 0; s < S; ++s) {
-        const uint32_t item = s * P + q;
-        const float4 tm = term[item];
-        v3 L = mk(tm.x, tm.y, tm.z);
-        const uint32_t mask = __float_as_uint(tm.w);
-        for (int slot = (int)max_bounce - 1; slot >= 0; --slot) {
-            if ((mask >> slot) & 1u) {
-                const float4 e = stk[(2ull * slot) * T + item];
-                const float2 a = reinterpret_cast<const float2*>(stk + (2ull * slot + 1) * T)[item];
-                L = add(mk(e.x, e.y, e.z), mul(mk(e.w, a.x, a.y), L));
+    if (tid < np && !first) { const float4 a = acc[q]; px = mk(a.x, a.y, a.z); }
+    for (uint32_t c = 0; c < S; c += kResSmp) {
+        const uint32_t ns = min(kResSmp, S - c);
+        for (uint32_t m = tid; m < kResPix * kResSmp; m += kBlock) {
+            const uint32_t i = m / kResSmp, k = m % kResSmp;   // the block's pixel i, sample c + k
+            if (i < np && k < ns) {
+                const uint32_t item = (q0 + i) * S + c + k;
+                const float4 tm = term[item];
+                v3 L = mk(tm.x, tm.y, tm.z);
+                const uint32_t mask = __float_as_uint(tm.w);
+                for (int slot = (int)max_bounce - 1; slot >= 0; --slot) {
+                    if ((mask >> slot) & 1u) {
+                        const float4 e = stk4[(uint64_t)slot * T + item];
+                        const float2 a = stk2[(uint64_t)slot * T + item];
+                        L = add(mk(e.x, e.y, e.z), mul(mk(e.w, a.x, a.y), L));
+                    }
+                }
+                float* dst = s_l + i * kResRow + 3u * k;
+                dst[0] = L.x; dst[1] = L.y; dst[2] = L.z;
             }
         }
-        px = add(px, L);
+        __syncthreads();
+        if (tid < np) {
+            const float* src = s_l + tid * kResRow;
+            for (uint32_t k = 0; k < ns; ++k) px = add(px, mk(src[3 * k], src[3 * k + 1], src[3 * k + 2]));
+        }
+        __syncthreads();
     }
+    if (tid >= np) return;
     if (!last) { acc[q] = make_float4(px.x, px.y, px.z, 0.0f); return; }
     const v3 l = mul(px, mk(inv_spp, inv_spp, inv_spp));
     uint8_t c[3];
@@ -1285,7 +1317,7 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float4* __restric
     v3 px = mk(0, 0, 0);
     if (!first) { const float4 a = acc[q]; px = mk(a.x, a.y, a.z); }
     for (uint32_t s = 0; s < S; ++s) {
-        const float4 c = out[(size_t)s * P + q];
+        const float4 c = out[(size_t)q * S + s];          // pixel-major items
         px = add(px, mk(c.x, c.y, c.z));
     }
     if (!last) { acc[q] = make_float4(px.x, px.y, px.z, 0.0f); return; }
@@ -1419,7 +1451,8 @@ struct zrt_context {
         float4* q0 = nullptr; size_t q0_cap = 0;
         float4* q1 = nullptr; size_t q1_cap = 0;
         float4* term = nullptr; size_t term_cap = 0;
-        float4* stk = nullptr; size_t stk_cap = 0;
+        float4* stk4 = nullptr; size_t stk4_cap = 0;   // bounce planes: (e, a.x) per (slot, item)
+        float2* stk2 = nullptr; size_t stk2_cap = 0;   //   (a.y, a.z) per (slot, item)
         uint32_t* wfc = nullptr; size_t wfc_cap = 0;
         float4* hit = nullptr; size_t hit_cap = 0;
         hipEvent_t ev_join = nullptr;      // set k > 0: its last pass is done
@@ -1527,7 +1560,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (zrt_context::PassSet& ps : c->set) {
-        void* sb[] = {ps.q0, ps.q1, ps.term, ps.stk, ps.wfc, ps.hit};
+        void* sb[] = {ps.q0, ps.q1, ps.term, ps.stk4, ps.stk2, ps.wfc, ps.hit};
         for (void* b : sb)
             if (b) (void)hipFree(b);
         if (ps.ev_join) (void)hipEventDestroy(ps.ev_join);
@@ -2010,20 +2043,24 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
             c->ncells = resolution[0] * resolution[1] * resolution[2];
             c->nrefs = dg.refs;
             c->d_cells = dg.cells;
+            c->d_data = dg.data;               // the context owns both from here (freed by destroy)
             if (kTriFloats == 12) {
                 c->d_pos = reinterpret_cast<float*>(dg.pos);
             } else {   // the device bake writes 3 float4 per ref: repack to 9 floats
-                HIP_TRY(hipMalloc((void**)&c->d_pos, 36ull * std::max<uint32_t>(dg.refs, 1)));
-                if (dg.refs) {
-                    hipLaunchKernelGGL(tri_repack_kernel, dim3((dg.refs + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                                       c->stream, (const float4*)dg.pos, dg.refs, c->d_pos);
-                    HIP_TRY(hipGetLastError());
-                    HIP_TRY(hipStreamSynchronize(c->stream));
-                }
-                (void)hipFree(dg.pos);
+                auto repack = [&]() -> int {
+                    HIP_TRY(hipMalloc((void**)&c->d_pos, 36ull * std::max<uint32_t>(dg.refs, 1)));
+                    if (dg.refs) {
+                        hipLaunchKernelGGL(tri_repack_kernel, dim3((dg.refs + kBlock - 1) / kBlock), dim3(kBlock),
+                                           0, c->stream, (const float4*)dg.pos, dg.refs, c->d_pos);
+                        HIP_TRY(hipGetLastError());
+                        HIP_TRY(hipStreamSynchronize(c->stream));
+                    }
+                    return ZRT_OK;
+                };
+                rc = repack();
+                (void)hipFree(dg.pos);         // on every path: the context never owned it
             }
-            c->d_data = dg.data;
-            if ((rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
+            if (rc == ZRT_OK && (rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
         }
     }
     if (rc != ZRT_OK) { zrt_context_destroy(c); return rc; }
@@ -2136,10 +2173,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const uint32_t mb = cfg->max_bounce;
     const uint32_t nb = std::max<uint32_t>(mb, 1);
     // per-item bytes of a pass: counting megakernel = the float4 sample
-    // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 32 B per
-    // bounce slot
-    // (+ the 16 B hit record the park kernel hands the shade kernel)
-    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 32ull * nb;
+    // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 24 B per
+    // bounce slot (+ the 16 B hit record the park kernel hands the shade kernel)
+    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 24ull * nb;
     // small frames run one set: a second stream costs its first launches
     // (the zrt CLI's 3-spp 1080p frame rendered in 30-39 vs 12.5-13.3 ms on a
     // fresh process) and does not pay back (cfg3 at 3 spp, warm: 7.1 vs 6.8
@@ -2152,7 +2188,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const bool ktimes = (cfg->flags & ZRT_FLAG_KERNEL_TIMES) != 0;
     size_t held = 16ull * c->out_cap;
     for (const zrt_context::PassSet& ps : c->set)
-        held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk_cap + ps.hit_cap) + 4ull * ps.wfc_cap;
+        held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk4_cap + ps.hit_cap) + 8ull * ps.stk2_cap +
+                4ull * ps.wfc_cap;
     const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets, held);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     // pass sets: pass p runs on set p % nsets, each set with its own stream
@@ -2191,7 +2228,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&ps.q0, &ps.q0_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.q1, &ps.q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.term, &ps.term_cap, T)) != ZRT_OK) return rc;
-        if ((rc = grow(&ps.stk, &ps.stk_cap, 2 * T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.stk4, &ps.stk4_cap, T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.stk2, &ps.stk2_cap, T * nb)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.wfc, &ps.wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
         if (k == 0) {
             ps.stream = c->stream;
@@ -2255,7 +2293,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // launch writes (round 2's counting render once wrote through an
     // unallocated d_out after a refactor of the pass logic; a stale, smaller
     // buffer must not pass silently either).  Queues 3 float4 per item, bounce
-    // planes 2 per (slot, item), terminal radiance / hit records / counting
+    // planes a float4 + a float2 per (slot, item), terminal radiance / hit records / counting
     // output 1 per item, the pass's items S * P <= T (checked per pass).
     {
         auto shortfall = [&](const char* what, const void* ptr, size_t cap, uint64_t need) {
@@ -2272,7 +2310,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         for (uint32_t k = 0; k < nsets && !counting && !bad; ++k) {
             const zrt_context::PassSet& ps = c->set[k];
             bad = shortfall("q0", ps.q0, ps.q0_cap, 3 * T) || shortfall("q1", ps.q1, ps.q1_cap, 3 * T) ||
-                  shortfall("term", ps.term, ps.term_cap, T) || shortfall("planes", ps.stk, ps.stk_cap, 2 * T * nb) ||
+                  shortfall("term", ps.term, ps.term_cap, T) || shortfall("planes4", ps.stk4, ps.stk4_cap, T * nb) ||
+                  shortfall("planes2", ps.stk2, ps.stk2_cap, T * nb) ||
                   shortfall("counters", ps.wfc, ps.wfc_cap, 24ull * kCtr * (mb + 2)) ||
                   (park_next && shortfall("hit records", ps.hit, ps.hit_cap, T)) ||
                   (k > 0 && (!ps.stream || !ps.ev_join));
@@ -2395,13 +2434,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         float4* const q0 = ps.q0;
         float4* const q1 = ps.q1;
         float4* const term = ps.term;
-        float4* const stk = ps.stk;
+        float4* const stk4 = ps.stk4;
+        float2* const stk2 = ps.stk2;
         uint32_t* const wfc = ps.wfc;
         float4* const hit = ps.hit;
         const uint32_t s0 = pass_first(pass);
         const uint32_t S = pass_count(pass);
         tp.s0 = s0;
         tp.total = S * P;
+        tp.S = S;
+        tp.sdiv = div_magic(S);
         const int first = pass == 0 ? 1 : 0, last = pass + 1 == npasses ? 1 : 0;
         if (!counting) {
             // per launch k: 8 work counters, then 8 region counts of the
@@ -2410,7 +2452,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             WfParams W;
             memset(&W, 0, sizeof W);
             W.t = tp;
-            W.stk = stk;
+            W.stk4 = stk4;
+            W.stk2 = stk2;
             W.term = term;
             W.T = (uint32_t)T;
             W.occx = c->d_occx;
@@ -2453,8 +2496,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             // the passes' sums into acc stay in pass order (stage3.zig:236-242)
             if (nsets > 1 && pass > 0) HIP_TRY(hipStreamWaitEvent(sm, c->ev_pass[pass - 1], 0));
             if ((rc = kt_begin(ZRT_KERNEL_RESOLVE, sm)) != ZRT_OK) return rc;
-            hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, sm,
-                               term, stk, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
+            hipLaunchKernelGGL(wf_resolve_kernel, dim3((P + kResPix - 1) / kResPix), dim3(kBlock), 0, sm,
+                               term, stk4, stk2, (uint32_t)T, P, S, mb, c->d_acc, first, last, inv_spp,
                                c->d_rgb, want_lin ? c->d_lin : nullptr);
             if ((rc = kt_end(sm)) != ZRT_OK) return rc;
             ++kp.launches[ZRT_KERNEL_RESOLVE];
