@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ZRT_ABI_VERSION 1
+#define ZRT_ABI_VERSION 2      /* 2: device list in zrt_render_config, zrt_group_* */
 
 typedef enum zrt_status {
     ZRT_OK = 0,
@@ -107,7 +107,14 @@ typedef struct zrt_render_config {
     uint32_t samples_per_pass;       /* samples of every pixel per device pass, 0 = automatic: as few
                                         passes as 144 GiB of path queues allow, at least two for frames
                                         of 2^23 samples or more (the image is the same for any value) */
-    uint32_t _reserved[4];
+    /* zrt_render only (ABI 2, in what were reserved words; zero = `device`
+     * alone): the image's tiles split over num_devices HIP ordinals, tile t
+     * rendered on devices[t % num_devices] (repeats allowed), gathered into
+     * rgb_out over xGMI -- the multi-device fan-out and join that
+     * Scene.render does with its worker threads (stage3.zig:247-256). */
+    uint32_t num_devices;
+    uint32_t _reserved0;
+    const int32_t* devices;
 } zrt_render_config;
 
 #define ZRT_FLAG_COUNT_STATS  0x1u   /* count cells/tests/hits (slower kernel variant) */
@@ -169,8 +176,11 @@ void zrt_geometry_free(zrt_geometry* g);
 /* ---- stage 3: the render seam ------------------------------------------ */
 
 /* One-shot drop-in for Scene.render: uploads the scene, renders the whole
- * image (rank 0 of 1) on `cfg->device`, writes w*h*3 RGB8 into rgb_out
- * (caller-allocated, row 0 = top), frees device memory, returns. */
+ * image on `cfg->device` -- or, with cfg->num_devices > 1, on every device of
+ * cfg->devices (one host thread and one context per entry, interleaved 64x64
+ * tiles, the packed tiles gathered to the first device over xGMI) -- writes
+ * w*h*3 RGB8 into rgb_out (caller-allocated, row 0 = top), frees device
+ * memory, returns.  The image is bit-identical for any device list. */
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_render_config* cfg,
                uint8_t* rgb_out, zrt_stats* stats);
 
@@ -200,6 +210,31 @@ int zrt_context_create_built(const float* positions, const float* normals, const
 int zrt_context_render(zrt_context* ctx, const zrt_camera* camera, const zrt_render_config* cfg,
                        const zrt_outputs* outputs, zrt_stats* stats);
 void zrt_context_destroy(zrt_context* ctx);
+
+/* A device group: one context per entry of `devices` (HIP ordinals, repeats
+ * allowed), the scene resident on each, rendered by one call -- Scene.render's
+ * spawn + join of its workers (stage3.zig:247-256) across GPUs in one
+ * process.  zrt_group_render splits this process's share of the image (the
+ * tiles t with t % cfg->num_ranks == cfg->rank; cfg->device is ignored) over
+ * the devices, device i taking sub-rank i, on one host thread each; with
+ * num_ranks <= 1 the devices' packed tiles are copied to devices[0] (peer copy
+ * over xGMI), scattered into the image there and copied to rgb_out once,
+ * otherwise each device's pixels are written into rgb_out from the host (other
+ * pixels untouched).  stats: sums over devices; render_ms = the slowest. */
+typedef struct zrt_group zrt_group;
+int zrt_group_create(const zrt_scene* scene, const int32_t* devices, uint32_t num_devices, zrt_group** out);
+/* Geometry.build + bakeInto on every device of the group (as
+ * zrt_context_create_built; the builds run in parallel, bit-identical). */
+int zrt_group_create_built(const float* positions, const float* normals, const float* texcoords,
+                           const uint32_t* material, uint32_t num_triangles, const uint32_t resolution[3],
+                           uint32_t num_materials, const zrt_material* materials, const float* texels,
+                           uint64_t num_texel_floats, const int32_t* devices, uint32_t num_devices,
+                           zrt_group** out);
+int zrt_group_render(zrt_group* g, const zrt_camera* camera, const zrt_render_config* cfg, uint8_t* rgb_out,
+                     zrt_stats* stats);
+/* The group's i-th context (owned by the group), e.g. for zrt_context_grid_info. */
+int zrt_group_context(zrt_group* g, uint32_t i, zrt_context** out);
+void zrt_group_destroy(zrt_group* g);
 
 /* Per-kernel breakdown of the context's last zrt_context_render (bench.py's
  * roofline: the dominant kernel's launch time and algorithmic work).

@@ -52,6 +52,59 @@ def test_oneshot_zrt_render_matches_golden(name):
     assert st["segments"] == int(g["counters"][0])
 
 
+def _golden_scene(name):
+    g = np.load(os.path.join(GOLD, f"render_{name}.npz"), allow_pickle=False)
+    soup = scenes.get_scene(name)
+    cname = str(g["camera"]) or None
+    c = soup.camera(cname)
+    cam = camera_for(soup, cname, None if c.aspect else int(g["w"]), int(g["h"]))
+    return g, soup, cam
+
+
+@pytest.mark.parametrize("name,devices", [("contest", [0, 0]), ("cornell", [0, 0, 0]), ("sphere", [0, 0])])
+def test_oneshot_zrt_render_device_list_matches_golden(name, devices):
+    """zrt_render with a device list (zrt_render_config.devices): the tiles
+    split over one context per entry (two or three contexts sharing GPU 0
+    here; the 8-GPU node is the driver's), gathered on the first device,
+    equal the golden one-device image bit for bit (stage3.zig:247-256 spawns
+    and joins every worker inside the one call)."""
+    g, soup, cam = _golden_scene(name)
+    geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
+    keep = []
+    native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
+    img, st = native.render_oneshot(geo.scene, cam, int(g["spp"]), int(g["max_bounce"]), seed=int(g["seed"]),
+                                    devices=devices)
+    assert np.array_equal(img.reshape(-1, 3), g["rgb"])
+    assert st["samples"] == cam.w * cam.h * int(g["spp"])
+    assert st["segments"] == int(g["counters"][0])
+
+
+def test_group_built_and_rank_share():
+    """zrt_group_create_built (the grid built on every device of the group)
+    renders the golden image; with num_ranks 2 the group renders only this
+    process's tiles (rank 1), each device a sub-rank, and leaves the other
+    pixels of the caller's image untouched."""
+    g, soup, cam = _golden_scene("contest")
+    mats = native.Scene()
+    keep = []
+    native.attach_materials(mats, soup.tex_desc, soup.texels, keep)
+    grp = native.Group.built(soup.pos, soup.nrm, soup.uv, soup.mat, mats, [0, 0])
+    try:
+        img, st = grp.render(cam, int(g["spp"]), int(g["max_bounce"]), seed=int(g["seed"]))
+        assert np.array_equal(img.reshape(-1, 3), g["rgb"])
+        assert st["segments"] == int(g["counters"][0])
+        part = np.full((cam.h, cam.w, 3), 7, np.uint8)
+        grp.render(cam, int(g["spp"]), int(g["max_bounce"]), seed=int(g["seed"]), rank=1, num_ranks=2, image=part)
+    finally:
+        grp.close()
+    mine = native.tile_pixels(cam.w, cam.h, 64, 1, 2)
+    flat = part.reshape(-1, 3)
+    assert np.array_equal(flat[mine], g["rgb"][mine])
+    other = np.ones(cam.w * cam.h, bool)
+    other[mine] = False
+    assert (flat[other] == 7).all()
+
+
 def test_oneshot_zrt_render_rejects_bad_input():
     soup = scenes.get_scene("sphere")
     geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat, resolution=(8, 8, 8))
@@ -63,6 +116,9 @@ def test_oneshot_zrt_render_rejects_bad_input():
     assert e.value.status == -1
     with pytest.raises(native.ZrtError) as e:
         native.render_oneshot(geo.scene, cam, 1, 4, device=99)
+    assert e.value.status == -2
+    with pytest.raises(native.ZrtError) as e:
+        native.render_oneshot(geo.scene, cam, 1, 4, devices=[0, 99])
     assert e.value.status == -2
 
 

@@ -147,14 +147,31 @@ def test_walk_loops_load_nothing_from_the_kernel_arguments(code):
     kernel-argument segment at a selected offset, waited on by a vmcnt(0) in
     every DDA step; the fields are laundered into registers now.  No timed
     kernel may form a vector address from the kernel-argument pointer
-    (s[0:1] at entry) inside a loop."""
+    (s[0:1] at entry) inside a loop -- unless the loop itself redefined
+    s[0:1] before that use (then it holds another pointer, e.g. one reloaded
+    from an SGPR spill lane)."""
     import re
     sc, ks = code
+    writes01 = re.compile(r"^\s*[sv]_\w+\s+(s\[0:1\]|s0|s1)\s*,")
     for sub in sc.timed():
         ins = _kernel(ks, sub)
         for b, e in _loops(ins):
-            bad = [t.strip() for _, t in ins[b:e + 1] if re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", t)]
+            body = [t.split("//")[0] for _, t in ins[b:e + 1]]
+            bad = [t.strip() for k, t in enumerate(body)
+                   if re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", t)
+                   and not any(writes01.search(x) for x in body[:k])]
             assert not bad, (sub, bad[:2])
+
+
+def test_kernel_argument_check_sees_a_kernarg_address():
+    """Control for the check above: a loop that forms an address from the
+    entry s[0:1] is caught, one that reloads s[0:1] first is not."""
+    import re
+    writes01 = re.compile(r"^\s*[sv]_\w+\s+(s\[0:1\]|s0|s1)\s*,")
+    use = "v_lshl_add_u64 v[0:1], s[0:1], 0, v[0:1]"
+    assert not any(writes01.search(x) for x in ["v_add_f32 v1, v1, v2"])
+    assert writes01.search("v_readlane_b32 s0, v70, 31") and writes01.search("s_load_dwordx2 s[0:1], s[4:5], 0x10")
+    assert re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", use)
 
 
 def ins_after(ins, e, n=40):

@@ -18,8 +18,18 @@ def test_abi_exports_every_declared_symbol():
     L = native.lib()
     missing = [s for s in sorted(declared) if not hasattr(L, s)]
     assert not missing, missing
-    assert L.zrt_abi_version() == 1
+    assert L.zrt_abi_version() == 2
     assert L.zrt_error_string(-5) == b"unsupported configuration"
+    assert set(native.EXPORTS) <= declared
+
+
+def test_render_config_layout_is_abi_stable():
+    """ABI 2 took the device list out of the reserved words: same size and
+    offsets of every ABI-1 field."""
+    import ctypes as C
+    rc = native.RenderConfig
+    assert C.sizeof(rc) == 56
+    assert rc.samples_per_pass.offset == 36 and rc.num_devices.offset == 40 and rc.devices.offset == 48
 
 
 @pytest.mark.parametrize("name,cam,w,h", [("sphere", None, 256, 256), ("cornell", None, 512, 512),

@@ -8,7 +8,8 @@
 // max_bounce), the same phase log lines on stderr ("info: Loaded in ...",
 // main.zig:103-142, durations printed like std.fmt.fmtDuration).  The render
 // phase runs the HIP path on every GPU listed in ZRT_DEVICES (default: device
-// 0); several GPUs split the image into interleaved tiles, one context each.
+// 0) through one libzrt device group (zrt_group_*): the image's interleaved
+// tiles split over the GPUs, one context each, gathered over xGMI.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -192,7 +193,11 @@ int main(int argc, char** argv) {
     zrt_camera cam;
     zrt_gltf* gltf = nullptr;
     zrt_geometry* geo = nullptr;
-    zrt_context* built = nullptr;   // one device: built there directly
+    zrt_group* group = nullptr;     // one context per device (zrt_group_*, libzrt)
+    struct GroupFree {
+        zrt_group*& g;
+        ~GroupFree() { zrt_group_destroy(g); }
+    } free_group{group};
     int rc;
     {
         const auto t = Clock::now();
@@ -211,26 +216,28 @@ int main(int argc, char** argv) {
         zrt_gltf_soup(gltf, &pos, &nrm, &uv, &mat, &ntri);
         info("Preprocessed in " + fmt_duration(since(t)));
     }
+    const uint32_t ndev = (uint32_t)devices.size();
     {
         const auto t = Clock::now();
         info("Grid resolution: { " + std::to_string(cfg.res[0]) + ", " + std::to_string(cfg.res[1]) + ", " +
              std::to_string(cfg.res[2]) + " }");
-        // One device (default): the grid is built on it straight into the
-        // render context (zrt_context_create_built, r01: 5-9 ms against
-        // 36-97 ms for host build + upload).  Several devices, or
-        // ZRT_DEVICE_BUILD=0: host threads, then one upload per device;
-        // ZRT_DEVICE_BUILD=1: device build with the host round trip.  Same
-        // arrays, bit for bit, on every path.
+        // Default: the grid is built on every render GPU straight into its
+        // context (zrt_group_create_built, the builds in parallel; r01: 5-9 ms
+        // against 36-97 ms for host build + upload).  ZRT_DEVICE_BUILD=0: host
+        // threads, then one upload per device; =1: device build with the host
+        // round trip.  Same arrays, bit for bit, on every path.
         const char* db = getenv("ZRT_DEVICE_BUILD");
-        const int mode = db ? atoi(db) : (devices.size() == 1 ? 2 : 0);
+        const int mode = db ? atoi(db) : 2;
         uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0, ncells = 0, nrefs = 0;
-        if (mode == 2 && devices.size() == 1) {
+        if (mode == 2) {
             if (hip_warm.joinable()) hip_warm.join();
-            rc = zrt_context_create_built(pos, nrm, uv, mat, ntri, cfg.res, scene.num_materials, scene.materials,
-                                          scene.texels, scene.num_texel_floats, devices[0], &built);
+            rc = zrt_group_create_built(pos, nrm, uv, mat, ntri, cfg.res, scene.num_materials, scene.materials,
+                                        scene.texels, scene.num_texel_floats, devices.data(), ndev, &group);
             if (rc != ZRT_OK) return fail("Geometry.build", rc);
+            zrt_context* c0 = nullptr;
             uint32_t gi[4];
-            if ((rc = zrt_context_grid_info(built, nullptr, gi)) != ZRT_OK) return fail("Geometry.build", rc);
+            if ((rc = zrt_group_context(group, 0, &c0)) != ZRT_OK || (rc = zrt_context_grid_info(c0, nullptr, gi)) != ZRT_OK)
+                return fail("Geometry.build", rc);
             ncells = cfg.res[0] * cfg.res[1] * cfg.res[2];
             nrefs = gi[0]; empty = gi[1]; mn = gi[2]; mx = gi[3];
         } else {
@@ -261,53 +268,32 @@ int main(int argc, char** argv) {
         info(buf);
         info("Compiled in " + fmt_duration(since(t)));
     }
-    std::vector<zrt_context*> ctx(devices.size(), nullptr);
-    {
+    if (!group) {
         const auto t = Clock::now();
         if (hip_warm.joinable()) hip_warm.join();
-        std::vector<int> rcs(devices.size(), ZRT_OK);
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < devices.size(); ++i)
-            th.emplace_back([&, i] {
-                if (built) ctx[i] = built;   // already on the device (one device)
-                else rcs[i] = zrt_context_create(&scene, devices[i], &ctx[i]);
-            });
-        for (auto& x : th) x.join();
-        for (int r : rcs)
-            if (r != ZRT_OK) return fail("zrt_context_create", r);
+        if ((rc = zrt_group_create(&scene, devices.data(), ndev, &group)) != ZRT_OK) return fail("zrt_group_create", rc);
         info("Uploaded in " + fmt_duration(since(t)));
     }
     std::vector<uint8_t> img((size_t)cam.w * cam.h * 3, 0);
     {
+        // Scene.render (main.zig:126): the image's tiles over the devices,
+        // one host thread each, gathered into img (zrt_group_render)
         const auto t = Clock::now();
-        std::vector<int> rcs(devices.size(), ZRT_OK);
-        std::vector<zrt_stats> st(devices.size());
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < devices.size(); ++i)
-            th.emplace_back([&, i] {
-                zrt_render_config rc_{};
-                rc_.num_samples = cfg.num_samples;
-                rc_.max_bounce = cfg.max_bounce;
-                rc_.device = devices[i];
-                rc_.rank = (uint32_t)i;
-                rc_.num_ranks = (uint32_t)devices.size();
-                zrt_outputs o{};
-                o.rgb_image = img.data();   // disjoint pixels per rank
-                rcs[i] = zrt_context_render(ctx[i], &cam, &rc_, &o, &st[i]);
-            });
-        for (auto& x : th) x.join();
-        for (int r : rcs)
-            if (r != ZRT_OK) return fail("Scene.render", r);
+        zrt_render_config rc_{};
+        rc_.num_samples = cfg.num_samples;
+        rc_.max_bounce = cfg.max_bounce;
+        rc_.num_ranks = 1;
+        zrt_stats st{};
+        if ((rc = zrt_group_render(group, &cam, &rc_, img.data(), &st)) != ZRT_OK) return fail("Scene.render", rc);
         const uint64_t ns = since(t);
-        uint64_t seg = 0;
-        for (const auto& s : st) seg += s.segments;
         info("Rendered in " + fmt_duration(ns));
         char buf[160];
-        snprintf(buf, sizeof buf, "Rays: %llu segments, %.1f Mrays/s on %zu GPU(s)", (unsigned long long)seg,
-                 seg / (ns / 1e9) / 1e6, devices.size());
+        snprintf(buf, sizeof buf, "Rays: %llu segments, %.1f Mrays/s on %u GPU(s)", (unsigned long long)st.segments,
+                 st.segments / (ns / 1e9) / 1e6, ndev);
         info(buf);
     }
-    for (zrt_context* c : ctx) zrt_context_destroy(c);
+    zrt_group_destroy(group);
+    group = nullptr;
     {
         const auto t = Clock::now();
         if ((rc = zrt_png_write(out.c_str(), img.data(), cam.w, cam.h)) != ZRT_OK) return fail("WritePngFail", rc);

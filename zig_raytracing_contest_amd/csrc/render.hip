@@ -2598,9 +2598,29 @@ extern "C" int zrt_context_profile(const zrt_context* c, zrt_kernel_profile* out
     return ZRT_OK;
 }
 
+int zrt::context_device_rgb(const zrt_context* c, const uint8_t** d_rgb, uint32_t* pixels, int* device) {
+    if (!c || !d_rgb || !pixels || !device) return ZRT_ERR_INVALID_ARG;
+    *d_rgb = c->d_rgb;
+    *pixels = c->pix_valid ? (uint32_t)c->pix.size() : 0u;
+    *device = c->device;
+    return ZRT_OK;
+}
+
 extern "C" int zrt_render(const zrt_scene* scene, const zrt_camera* cam, const zrt_render_config* cfg,
                           uint8_t* rgb_out, zrt_stats* stats) {
     if (!scene || !cam || !cfg || !rgb_out) return ZRT_ERR_INVALID_ARG;
+    if (cfg->num_devices > 1) {                // the image's tiles over a device list (group.hip)
+        if (!cfg->devices) return ZRT_ERR_INVALID_ARG;
+        zrt_group* g = nullptr;
+        int rc = zrt_group_create(scene, cfg->devices, cfg->num_devices, &g);
+        if (rc != ZRT_OK) return rc;
+        zrt_render_config whole = *cfg;
+        whole.rank = 0;
+        whole.num_ranks = 1;
+        rc = zrt_group_render(g, cam, &whole, rgb_out, stats);
+        zrt_group_destroy(g);
+        return rc;
+    }
     zrt_context* c = nullptr;
     int rc = zrt_context_create(scene, cfg->device, &c);
     if (rc != ZRT_OK) return rc;

@@ -39,4 +39,9 @@ inline bool occx_usable(uint64_t bricks, uint64_t occupied, uint64_t lds_bytes, 
 int tile_pixels(uint32_t w, uint32_t h, uint32_t tile, uint32_t rank, uint32_t nranks,
                 uint32_t* out, uint32_t* count);
 
+// The packed RGB8 of a context's last render (device memory on its device,
+// 3 * pixels bytes in its rank's zrt_tile_pixels order): what a device group
+// gathers (group.hip).
+int context_device_rgb(const zrt_context* c, const uint8_t** d_rgb, uint32_t* pixels, int* device);
+
 }  // namespace zrt

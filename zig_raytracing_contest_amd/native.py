@@ -74,7 +74,8 @@ class RenderConfig(C.Structure):
     _fields_ = [("num_samples", C.c_uint32), ("max_bounce", C.c_uint32), ("seed", C.c_uint64),
                 ("device", C.c_int32), ("rank", C.c_uint32), ("num_ranks", C.c_uint32),
                 ("tile_size", C.c_uint32), ("flags", C.c_uint32), ("samples_per_pass", C.c_uint32),
-                ("_reserved", C.c_uint32 * 4)]
+                ("num_devices", C.c_uint32), ("_reserved0", C.c_uint32),
+                ("devices", C.POINTER(C.c_int32))]
 
 
 class Stats(C.Structure):
@@ -111,6 +112,7 @@ EXPORTS = [
     "zrt_context_create", "zrt_context_create_built", "zrt_context_grid_info", "zrt_context_render", "zrt_context_destroy", "zrt_tile_pixels",
     "zrt_gltf_load", "zrt_gltf_soup", "zrt_gltf_materials", "zrt_gltf_camera", "zrt_gltf_free",
     "zrt_camera_from_matrix", "zrt_probe", "zrt_timed_kernels", "zrt_context_profile",
+    "zrt_group_create", "zrt_group_create_built", "zrt_group_render", "zrt_group_context", "zrt_group_destroy",
 ]
 
 
@@ -147,6 +149,16 @@ def lib():
     L.zrt_context_profile.argtypes = [C.c_void_p, C.POINTER(KernelProfile)]
     L.zrt_context_destroy.argtypes = [C.c_void_p]
     L.zrt_context_destroy.restype = None
+    L.zrt_group_create.argtypes = [C.POINTER(Scene), C.POINTER(C.c_int32), C.c_uint32, C.POINTER(C.c_void_p)]
+    L.zrt_group_create_built.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(Material),
+                                         C.POINTER(C.c_float), C.c_uint64, C.POINTER(C.c_int32), C.c_uint32,
+                                         C.POINTER(C.c_void_p)]
+    L.zrt_group_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig), C.c_void_p,
+                                   C.POINTER(Stats)]
+    L.zrt_group_context.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.zrt_group_destroy.argtypes = [C.c_void_p]
+    L.zrt_group_destroy.restype = None
     L.zrt_tile_pixels.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_void_p, C.POINTER(C.c_uint32)]
     L.zrt_camera_from_matrix.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int32,
@@ -345,17 +357,72 @@ class Context:
 
 
 def render_oneshot(scene: Scene, cam: Camera, spp: int, max_bounce: int, seed: int = 0,
-                   device: int = -1):
+                   device: int = -1, devices=None):
     """zrt_render: the one-shot drop-in for Scene.render (stage3.zig:247) --
-    upload, render the whole image, download, free.  Returns (h, w, 3) RGB8."""
+    upload, render the whole image, download, free.  `devices`: a list of
+    HIP ordinals (repeats allowed) to split the image's tiles over
+    (zrt_render_config.devices / num_devices).  Returns (h, w, 3) RGB8."""
     cfg = RenderConfig()
     cfg.num_samples, cfg.max_bounce, cfg.seed, cfg.device = spp, max_bounce, seed, device
     cfg.num_ranks = 1
+    if devices is not None:
+        dl = (C.c_int32 * len(devices))(*devices)
+        cfg.num_devices, cfg.devices = len(devices), dl
     img = np.zeros((cam.h, cam.w, 3), np.uint8)
     st = Stats()
     check(lib().zrt_render(C.byref(scene), C.byref(cam), C.byref(cfg), img.ctypes.data, C.byref(st)),
           "zrt_render")
     return img, st.as_dict()
+
+
+class Group:
+    """zrt_group: one context per device of `devices` (repeats allowed), one
+    render call splitting the image's tiles over them and gathering them over
+    xGMI into one image (Scene.render's spawn + join, stage3.zig:247-256)."""
+
+    def __init__(self, scene: Scene, devices):
+        self._dev = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        check(lib().zrt_group_create(C.byref(scene), self._dev, len(devices), C.byref(h)), "zrt_group_create")
+        self._h = h
+        self.devices = list(devices)
+
+    @classmethod
+    def built(cls, pos, nrm, uv, mat, materials: Scene, devices, resolution=(128, 128, 128)):
+        """zrt_group_create_built: the grid built on every device."""
+        keep = [np.ascontiguousarray(pos, np.float32), np.ascontiguousarray(nrm, np.float32),
+                np.ascontiguousarray(uv, np.float32), np.ascontiguousarray(mat, np.uint32)]
+        res = (C.c_uint32 * 3)(*resolution)
+        self = cls.__new__(cls)
+        self._dev = (C.c_int32 * len(devices))(*devices)
+        self.devices = list(devices)
+        h = C.c_void_p()
+        check(lib().zrt_group_create_built(*[k.ctypes.data for k in keep], keep[3].size, res,
+                                           materials.num_materials, materials.materials, materials.texels,
+                                           materials.num_texel_floats, self._dev, len(devices), C.byref(h)),
+              "zrt_group_create_built")
+        self._h = h
+        return self
+
+    def render(self, cam: Camera, spp: int, max_bounce: int, seed: int = 0, rank: int = 0, num_ranks: int = 1,
+               image=None, flags=0):
+        """Returns ((h, w, 3) RGB8 with this process's pixels, stats dict)."""
+        cfg = RenderConfig()
+        cfg.num_samples, cfg.max_bounce, cfg.seed = spp, max_bounce, seed
+        cfg.rank, cfg.num_ranks, cfg.flags = rank, num_ranks, flags
+        img = np.zeros((cam.h, cam.w, 3), np.uint8) if image is None else image
+        st = Stats()
+        check(lib().zrt_group_render(self._h, C.byref(cam), C.byref(cfg), img.ctypes.data, C.byref(st)),
+              "zrt_group_render")
+        return img, st.as_dict()
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.zrt_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def timed_kernels():
