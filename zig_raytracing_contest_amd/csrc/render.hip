@@ -308,9 +308,20 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
     return nearest;
 }
 
+// Texture(T).sample (stage3.zig:111-123).  A 1x1 texture -- the dummy of
+// every material slot without an image (stage1.zig:411-425) -- has all four
+// texel indices 0 (any clamp, @mod by 1), so it loads its texel once and
+// runs the same bilinear arithmetic on it (bit-identical: x - x is not
+// folded, NaN/inf weights propagate as before), instead of the index
+// arithmetic and four loads per channel.
 __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, float u, float v) {
-    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
     const float* b = texels + t.off;
+    if (t.w == 1 && t.h == 1) {
+        const float fu = tex_frac(u), fv = tex_frac(v);
+        const float x = b[0], y = b[1], z = b[2];
+        return mk(bilerp(x, x, x, x, fu, fv), bilerp(y, y, y, y, fu, fv), bilerp(z, z, z, z, fu, fv));
+    }
+    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
     v3 r;
     r.x = bilerp(b[3 * c.i11 + 0], b[3 * c.i21 + 0], b[3 * c.i12 + 0], b[3 * c.i22 + 0], c.fu, c.fv);
     r.y = bilerp(b[3 * c.i11 + 1], b[3 * c.i21 + 1], b[3 * c.i12 + 1], b[3 * c.i22 + 1], c.fu, c.fv);
@@ -318,8 +329,12 @@ __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, floa
     return r;
 }
 __device__ __forceinline__ float sample1(const float* texels, const DevTex& t, float u, float v) {
-    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
     const float* b = texels + t.off;
+    if (t.w == 1 && t.h == 1) {                           // the 1x1 dummy (see sample3)
+        const float x = b[0];
+        return bilerp(x, x, x, x, tex_frac(u), tex_frac(v));
+    }
+    const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
     return bilerp(b[c.i11], b[c.i21], b[c.i12], b[c.i22], c.fu, c.fv);
 }
 
@@ -523,25 +538,41 @@ __device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
 // path continues (o, d, depth, slot, rng, mask updated); false with L set
 // when it terminates.
 // `mats`: the material descriptors (p.mats, or the shade kernel's LDS copy).
+// `sp` (ZRT_SWEEP builds, the shade kernel only): per-wave s_memtime cycles
+// and active lanes of the phases (SHADE_STAMP), else null.
+#ifdef ZRT_SWEEP
+// phase k: cycles into sp[k], active lanes into sp[8 + k]; sp[16] the last tick.
+// `v`: a value the phase produced, so the stamp waits for it
+#define SHADE_STAMP(k, v) do { if (sp) { asm volatile("" :: "v"(v)); const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    sp[k] += t_ - sp[16]; sp[16] = t_; sp[8 + (k)] += (uint64_t)__popcll(__ballot(1)); } } while (0)
+#else
+#define SHADE_STAMP(k, v) do { (void)sp; } while (0)
+#endif
 __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* zx, const double* zf,
                                               const DevMat* mats, uint32_t item, float t, float hu, float hv,
                                               uint32_t hidx, v3& o, v3& d, uint32_t& depth, uint32_t& slot,
-                                              Rng& rng, uint32_t& mask, v3& L) {
+                                              Rng& rng, uint32_t& mask, v3& L,
+                                              unsigned long long* sp = nullptr) {
     const TraceParams& p = w.t;
+    SHADE_STAMP(1, t);                                      // the hit record landed
     if (t == kInf) { L = env_color(d); return false; }     // stage3.zig:195-197
     const float4* tdp = p.tri_data + 4ull * hidx;          // stage3.zig:199-206
     const float4 d0 = tdp[0], d1 = tdp[1], d2 = tdp[2], d3 = tdp[3];
     const float w0 = 1.0f - hu - hv;
     const float tc0 = (d2.y * w0 + d2.w * hu) + d3.y * hv;
     const float tc1 = (d2.z * w0 + d3.x * hu) + d3.z * hv;
+    SHADE_STAMP(2, tc1);                                    // triangle data
     const DevMat& m = mats[__float_as_uint(d3.w)];
     const v3 albedo = sample3(p.texels, m.tex[0], tc0, tc1);
     const v3 emissive = sample3(p.texels, m.tex[1], tc0, tc1);
     const float transparency = sample1(p.texels, m.tex[2], tc0, tc1);
+    SHADE_STAMP(3, transparency);                           // material + texels
     const v3 nrm = add(add(scale(mk(d0.x, d0.y, d0.z), w0), scale(mk(d0.w, d1.x, d1.y), hu)),
                        scale(mk(d1.z, d1.w, d2.x), hv));
     const v3 no = add(o, scale(d, t + kFltEps));
-    if (!(rng_float(rng) > transparency)) {                 // stage3.zig:207, :214-219
+    const float u_tr = rng_float(rng);
+    SHADE_STAMP(4, u_tr);                                   // transparency draw
+    if (!(u_tr > transparency)) {                           // stage3.zig:207, :214-219
         // the (e, a) pair goes out before the normal draws, so the ziggurat
         // (f64, 64-bit RNG) runs without the six colour registers live; 24 B
         // per pair instead of two float4 (r03zk: cfg3 +0.5%, cfg2 +1.6%,
@@ -553,6 +584,7 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
         const float nz = (float)rng_norm64(rng, zx, zf);
         d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
         mask |= 1u << slot;
+        SHADE_STAMP(5, d.x);                                // pair store + ziggurat draws
     }
     o = no;
     --depth;
@@ -1167,28 +1199,30 @@ __device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, 
                                            const DevMat* mats, bool valid,
                                            uint32_t item, v3 o, v3 d, uint32_t depth, uint32_t slot, Rng rng,
                                            uint32_t mask, float4 h, uint64_t below, uint32_t grp,
-                                           uint32_t& n_seg) {
+                                           uint32_t& n_seg, unsigned long long* sp = nullptr) {
     bool cont = false;
     if (valid) {
         v3 L = mk(0, 0, 0);
         ++n_seg;                               // queued / primary paths have depth >= 1
         cont = shade_segment(w, zx, zf, mats, item, h.x, h.y, h.z, __float_as_uint(h.w), o, d, depth, slot,
-                             rng, mask, L);
+                             rng, mask, L, sp);
         if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
     }
+    SHADE_STAMP(6, o.x);                       // the rest of the segment (misses, pass-through, terminal store)
     wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
+    SHADE_STAMP(7, o.x);                       // append
 }
 
 // One queue entry: its path record (a, b, c) and hit record h already loaded.
 __device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx, const double* zf,
                                             const DevMat* mats, bool valid,
                                             float4 a, float4 b, float4 c, float4 h, uint64_t below,
-                                            uint32_t grp, uint32_t& n_seg) {
+                                            uint32_t grp, uint32_t& n_seg, unsigned long long* sp = nullptr) {
     Rng rng;
     rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
     shade_path(w, zx, zf, mats, valid, __float_as_uint(a.w), mk(a.x, a.y, a.z), mk(b.x, b.y, b.z),
                __float_as_uint(b.w) & 0xFFFFu, __float_as_uint(b.w) >> 16, rng, __float_as_uint(c.z), h, below,
-               grp, n_seg);
+               grp, n_seg, sp);
 }
 
 // LMATS: the material descriptors (at most kLdsMats) copied to dynamic LDS
@@ -1221,6 +1255,15 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
     WfParams ws = w;
     ws.fetch8 = w.fetch8s;
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#ifdef ZRT_SWEEP
+    // ZRT_SWEEP builds: per-wave cycles and active lanes of the shading phases
+    // (SHADE_STAMP; printed as zrt_shade_profile with ZRT_PARK_PROFILE)
+    unsigned long long sprof[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    sprof[16] = __builtin_amdgcn_s_memtime();
+    unsigned long long* const sp = sprof;
+#else
+    unsigned long long* const sp = nullptr;
+#endif
     // kShadeEntries entries per lane per fetch: every entry's records are
     // loaded before the first is shaded, so their latency overlaps the
     // earlier entries' dependent chains (2: cfg3 +1.2%, cfg2 / cfg5 within
@@ -1228,6 +1271,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
     for (;;) {
         uint32_t base = 0, lim = 0;
         if (!wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim)) break;
+        SHADE_STAMP(0, base);                  // work atomic
         float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
 #pragma unroll
         for (int e = 0; e < kShadeEntries; ++e) {
@@ -1240,10 +1284,15 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
         }
 #pragma unroll
         for (int e = 0; e < kShadeEntries; ++e)
-            shade_entry(w, zx, zf, mats, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg);
+            shade_entry(w, zx, zf, mats, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg,
+                        sp);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
+#ifdef ZRT_SWEEP
+    if (lane == 0)
+        for (int k = 0; k < 16; ++k) atomicAdd(&p.stats[32 + k], sprof[k]);
+#endif
 }
 
 // Fold + ordered sample sum + toRGB for wavefront mode (stage3.zig:219,
@@ -1745,7 +1794,7 @@ static int context_counters(zrt_context* c) {
     int rc = context_packed(c);
     if (rc != ZRT_OK) return rc;
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
-    HIP_TRY(hipMalloc((void**)&c->d_stats, 256));
+    HIP_TRY(hipMalloc((void**)&c->d_stats, 512));
     return ZRT_OK;
 }
 
@@ -2420,7 +2469,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     };
     zrt_kernel_profile kp{};
 
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 256, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 512, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
     if (nsets > 1) {                           // the other sets start after the stats reset
         HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
@@ -2531,7 +2580,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                                c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
 
-    unsigned long long hs[32];
+    unsigned long long hs[64];
     HIP_TRY(hipMemcpy(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost));
     // diagnostics (debugging only): counting-build walk/test trip counts,
     // per-launch device times
@@ -2550,6 +2599,12 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);
+    if (getenv("ZRT_PARK_PROFILE") && park_next)   // wf_shade_kernel phases: wave cycles, active-lane sums
+        fprintf(stderr, "{\"zrt_shade_profile\": {\"cyc\": [%llu, %llu, %llu, %llu, %llu, %llu, %llu, %llu], "
+                "\"lanes\": [%llu, %llu, %llu, %llu, %llu, %llu, %llu, %llu], \"phases\": [\"fetch\", \"records\", "
+                "\"tri_data\", \"texels\", \"u_draw\", \"pair_ziggurat\", \"tail\", \"append\"]}}\n",
+                hs[32], hs[33], hs[34], hs[35], hs[36], hs[37], hs[38], hs[39], hs[40], hs[41], hs[42], hs[43],
+                hs[44], hs[45], hs[46], hs[47]);
 #endif
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_begin, c->ev_end));
