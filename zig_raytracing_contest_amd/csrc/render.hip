@@ -76,6 +76,10 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
+// ZRT_SPATIAL: bounce queues binned by origin octant (measured variant, off)
+#ifndef ZRT_SPATIAL
+#define ZRT_SPATIAL 0
+#endif
 // DDA steps per park walk trip, every cell's brick lookup in flight at once
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
 // +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
@@ -519,6 +523,15 @@ struct WfParams {
     uint32_t occx_ldsw;       // u32 words OccX takes in LDS (multiple of 4): entries + masks
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
+    // ZRT_SPATIAL (measured variant): bounce queues binned by
+    // the octant of the next segment's origin around spl[] instead of by pixel
+    // range; region g of a binned queue starts at the prefix of the per-octant
+    // counts the launch's park kernel histogrammed (hist), so it needs no
+    // per-region capacity
+    uint32_t spatial_in, spatial_out;     // q_in / q_out binned by octant
+    const uint32_t* hist_in;              // counts per region of q_in (binned)
+    uint32_t* hist_out;                   // park kernel: counts per region the shade kernel appends
+    float spl[3];
 };
 
 // Work / append counters: one per 128-byte line (32 u32), so the waves'
@@ -530,6 +543,19 @@ constexpr uint32_t kCtr = 32;
 __device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
     const uint32_t nblk = (P + 63u) >> 6;
     return min(P, (nblk * g / 8u) * 64u);
+}
+
+// First queue entry of region g: pixel-range regions at S * (first pixel),
+// octant-binned ones at the prefix of the launch's per-region counts.
+__device__ __forceinline__ uint32_t region_base(const WfParams& w, uint32_t binned, const uint32_t* hist, uint32_t g) {
+    if (!ZRT_SPATIAL || !binned) return w.t.S * xcd_q0(w.t.P, g);
+    uint32_t b = 0;
+    for (uint32_t h = 0; h < g; ++h) b += hist[h * kCtr];
+    return b;
+}
+// The octant (region) of a next-segment origin.
+__device__ __forceinline__ uint32_t origin_bin(const WfParams& w, v3 no) {
+    return (no.x >= w.spl[0] ? 1u : 0u) | (no.y >= w.spl[1] ? 2u : 0u) | (no.z >= w.spl[2] ? 4u : 0u);
 }
 
 // traceRayRecursive's body after the hit (stage3.zig:195-219) for one
@@ -602,12 +628,12 @@ __device__ __forceinline__ void q_store(const WfParams& w, uint32_t pos, v3 o, v
 }
 
 // Append the continuing paths of the wave (lanes with `cont`) to the next
-// queue, each to the region `reg` of its pixel range: one returning atomic
-// per distinct region of the wave, ranks from ballot + popcount.
+// queue, each to the region `reg` (its pixel range; ZRT_SPATIAL: its origin's
+// octant): one returning atomic per distinct region of the wave, ranks from
+// ballot + popcount.
 __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d, uint32_t item,
                                           uint32_t depth, uint32_t slot, const Rng& rng, uint32_t mask,
                                           uint32_t reg) {
-    const uint32_t S = w.t.S;
     uint64_t pend = __ballot(cont);
     while (pend) {
         const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
@@ -615,7 +641,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
         const uint64_t m = __ballot(cont && reg == g);
         uint32_t ob = 0;
         if ((threadIdx.x & 63u) == lead) ob = atomicAdd(&w.n_out8[g * kCtr], (uint32_t)__popcll(m));
-        ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)lead) + S * xcd_q0(w.t.P, g);
+        ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)lead) + region_base(w, w.spatial_out, w.hist_out, g);
         if (cont && reg == g) q_store(w, ob + (uint32_t)__popcll(m & below), o, d, item, depth, slot, rng, mask);
         pend &= ~m;
     }
@@ -657,8 +683,9 @@ __device__ __forceinline__ bool wf_fetch(const WfParams& w, uint32_t want, uint3
 // apart: 126 B of DRAM writes per primary item for <= 72 B of records, r03zm).
 // Bounce launches: entry j of region g is queue index S * q0 + j.
 template <bool PRIMARY>
-__device__ __forceinline__ uint32_t ent_index(const TraceParams& p, uint32_t grp, uint32_t j) {
-    return p.S * xcd_q0(p.P, grp) + j;
+__device__ __forceinline__ uint32_t ent_index(const WfParams& w, uint32_t grp, uint32_t j) {
+    if (PRIMARY) return w.t.S * xcd_q0(w.t.P, grp) + j;
+    return region_base(w, w.spatial_in, w.hist_in, grp) + j;
 }
 
 // The path state of queue entry / primary item `i` that shading needs.
@@ -712,7 +739,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
       for (uint32_t sub = 0; sub < kWfChunk && base + 64u * sub < lim; ++sub) {
         const uint32_t j = base + 64u * sub + lane;
         const bool valid = j < lim;
-        const uint32_t i = valid ? ent_index<PRIMARY>(p, grp, j) : 0u;
+        const uint32_t i = valid ? ent_index<PRIMARY>(w, grp, j) : 0u;
         bool cont = false;
         uint32_t mask = 0, r_item = 0, r_depth = 0, r_slot = 0;
         v3 r_o = mk(0, 0, 0), r_d = mk(0, 0, 0);
@@ -978,6 +1005,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
+    uint32_t pdepth = 0;                   // its depth (ZRT_SPATIAL's histogram)
     PARK_PROF_DECL
 
     for (;;) {
@@ -992,9 +1020,24 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // data registers with a vmcnt(0) INSIDE the loop, which then
                 // also waits for the previous step's range load, every step
                 // (r02f ISA; walk 1304 cycles per step)
-                if (st == kDone) {
+                const bool done = st == kDone;
+                if (done) {
                     w.hit[qi] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
                     st = kIdle;
+                }
+                if (ZRT_SPATIAL && w.spatial_out) {            // octant histogram of the paths the
+                    // shade kernel will append: hits with depth left, binned by
+                    // the origin it will compute (the same f32 arithmetic)
+                    const bool app = done && nearest != kInf && pdepth > 1u;
+                    const uint32_t bin = origin_bin(w, add(o, scale(d, nearest + kFltEps)));
+                    uint64_t pend = __ballot(app);
+                    while (pend) {
+                        const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
+                        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
+                        const uint64_t m = __ballot(app && bin == g);
+                        if (lane == lead) atomicAdd(&w.hist_out[g * kCtr], (uint32_t)__popcll(m));
+                        pend &= ~m;
+                    }
                 }
                 __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
@@ -1017,11 +1060,12 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const uint32_t rank = (uint32_t)__popcll(idle & below);
                 if (st == kIdle && rank < take) {
                     {
-                        qi = ent_index<false>(p, cgrp, cb + rank);
+                        qi = ent_index<false>(w, cgrp, cb + rank);
                         {
                             const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
                             o = mk(qa.x, qa.y, qa.z);
                             d = mk(qb.x, qb.y, qb.z);
+                            pdepth = __float_as_uint(qb.w) & 0xFFFFu;
                         }
                         {                                          // queued paths have depth >= 1
                             nearest = kInf;
@@ -1209,7 +1253,7 @@ __device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, 
         if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
     }
     SHADE_STAMP(6, o.x);                       // the rest of the segment (misses, pass-through, terminal store)
-    wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
+    wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, ZRT_SPATIAL && w.spatial_out ? origin_bin(w, o) : grp);
     SHADE_STAMP(7, o.x);                       // append
 }
 
@@ -1278,7 +1322,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
             const uint32_t j = base + 64u * e + lane;
             a[e] = b[e] = c[e] = h[e] = z4;
             if (j < lim) {
-                const uint32_t i = ent_index<false>(p, grp, j);
+                const uint32_t i = ent_index<false>(w, grp, j);
                 a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2]; h[e] = w.hit[i];
             }
         }
@@ -1490,6 +1534,7 @@ struct zrt_context {
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
+    float spl[3] = {0.0f, 0.0f, 0.0f};  // ZRT_SPATIAL: octant split point (median ref v0)
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;     // counting build
@@ -1827,6 +1872,14 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
     HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
+    if (ZRT_SPATIAL && c->nrefs) {             // octant split: the refs' median v0 per axis
+        std::vector<float> v(c->nrefs);
+        for (int a = 0; a < 3; ++a) {
+            for (uint32_t i = 0; i < c->nrefs; ++i) v[i] = s->triangles_pos[9ull * i + a];
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            c->spl[a] = v[v.size() / 2];
+        }
+    }
     if ((rc = context_materials(c, s)) != ZRT_OK) return rc;
     return context_occupancy(c, s->cells);
 }
@@ -2279,7 +2332,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&ps.term, &ps.term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.stk4, &ps.stk4_cap, T * nb)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.stk2, &ps.stk2_cap, T * nb)) != ZRT_OK) return rc;
-        if ((rc = grow(&ps.wfc, &ps.wfc_cap, 24ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.wfc, &ps.wfc_cap, 32ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
         if (k == 0) {
             ps.stream = c->stream;
         } else {
@@ -2331,6 +2384,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     const bool packed = c->packed;
+    const bool spatial = ZRT_SPATIAL && park_next;   // binned queues need the park kernel's histogram
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
@@ -2361,7 +2415,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             bad = shortfall("q0", ps.q0, ps.q0_cap, 3 * T) || shortfall("q1", ps.q1, ps.q1_cap, 3 * T) ||
                   shortfall("term", ps.term, ps.term_cap, T) || shortfall("planes4", ps.stk4, ps.stk4_cap, T * nb) ||
                   shortfall("planes2", ps.stk2, ps.stk2_cap, T * nb) ||
-                  shortfall("counters", ps.wfc, ps.wfc_cap, 24ull * kCtr * (mb + 2)) ||
+                  shortfall("counters", ps.wfc, ps.wfc_cap, 32ull * kCtr * (mb + 2)) ||
                   (park_next && shortfall("hit records", ps.hit, ps.hit_cap, T)) ||
                   (k > 0 && (!ps.stream || !ps.ev_join));
         }
@@ -2497,7 +2551,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if (!counting) {
             // per launch k: 8 work counters, then 8 region counts of the
             // paths entering launch k (written by launch k - 1)
-            HIP_TRY(hipMemsetAsync(wfc, 0, 4ull * 24 * kCtr * (mb + 2), sm));
+            HIP_TRY(hipMemsetAsync(wfc, 0, 4ull * 32 * kCtr * (mb + 2), sm));
             WfParams W;
             memset(&W, 0, sizeof W);
             W.t = tp;
@@ -2522,6 +2576,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.n_out8 = wfc + kCtr * (16 * (k + 1) + 8);
                 W.hit = hit;
                 W.fetch8s = wfc + kCtr * (16 * (mb + 2) + 8 * k);
+                // ZRT_SPATIAL: the shade half of launch k >= 1 appends by octant
+                // (histogrammed by its park half); launch k + 1 reads those regions
+                W.spatial_out = spatial && k >= 1;
+                W.spatial_in = spatial && k >= 2;
+                W.hist_out = wfc + kCtr * (24 * (mb + 2) + 8 * k);
+                W.hist_in = k ? wfc + kCtr * (24 * (mb + 2) + 8 * (k - 1)) : nullptr;
+                for (int a = 0; a < 3; ++a) W.spl[a] = c->spl[a];
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 const int cls = k == 0 ? ZRT_KERNEL_PRIMARY : (park_next ? ZRT_KERNEL_PARK : ZRT_KERNEL_BOUNCE);
                 if ((rc = kt_begin(cls, sm)) != ZRT_OK) return rc;
