@@ -76,6 +76,14 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
+// ZRT_OCCX8: the park kernel's LDS OccX holds an 8-bit mask of occupied 2^3
+// sub-bricks per occupied 4^3 brick instead of the 64-bit cell mask (~47 KB
+// less LDS on the contest stand-in); a lane then parks in any cell of an
+// occupied sub-brick and an empty range unparks it at the next trip
+// (measured variant, off)
+#ifndef ZRT_OCCX8
+#define ZRT_OCCX8 0
+#endif
 // ZRT_SPATIAL: bounce queues binned by origin octant (measured variant, off)
 #ifndef ZRT_SPATIAL
 #define ZRT_SPATIAL 0
@@ -188,6 +196,10 @@ __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uin
 // and masks.)
 __device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
     const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
+    if (ZRT_OCCX8) {   // sub-brick ((x >> 1) & 1) | ((y >> 1) & 1) << 1 | ((z >> 1) & 1) << 2
+        const uint32_t sb = ((i >> 1) & 1u) | ((i >> 2) & 2u) | ((i >> 3) & 4u);
+        return ((uint32_t)bm >> sb) & 1u;
+    }
     return (uint32_t)(bm >> (i & 63u)) & 1u;
 }
 
@@ -833,11 +845,24 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 struct OccX {
     const uint2* ent;                    // (brick bits, 1 + occupied bricks before the word)
     const unsigned long long* masks;     // [0]: zero mask
+    const uint8_t* masks8;               // ZRT_OCCX8: sub-brick masks, [0] zero
 };
 __device__ __forceinline__ unsigned long long occx_mask_at(const OccX& L, uint2 e, uint32_t b) {
     const uint32_t low = __builtin_amdgcn_ubfe(e.x, 0u, b);        // bits of the bricks below b
     const uint32_t bit = __builtin_amdgcn_ubfe(e.x, b, 1u);
+    if (ZRT_OCCX8) return L.masks8[__umul24((uint32_t)__popc(low) + e.y, bit)];
     return L.masks[__umul24((uint32_t)__popc(low) + e.y, bit)];
+}
+// a 64-bit cell mask -> its 8-bit sub-brick mask (ZRT_OCCX8)
+__device__ __forceinline__ uint32_t occx_sub8(unsigned long long m) {
+    uint32_t r = 0;
+    for (uint32_t sb = 0; sb < 8; ++sb) {
+        const uint32_t x = (sb & 1u) << 1, y = sb & 2u, z = (sb >> 1) & 2u;   // sub-brick origin cell
+        const uint32_t i0 = x | (y << 2) | (z << 4);
+        const unsigned long long sub = (3ull << i0) | (3ull << (i0 + 4)) | (3ull << (i0 + 16)) | (3ull << (i0 + 20));
+        r |= (m & sub) ? (1u << sb) : 0u;
+    }
+    return r;
 }
 __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
     return occx_mask_at(L, L.ent[b >> 5], b);
@@ -977,13 +1002,21 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
         uint2* ent = reinterpret_cast<uint2*>(s_dyn);
         for (uint32_t i = threadIdx.x; i < w.occx_nbw; i += blockDim.x) ent[i] = make_uint2(w.occx[i], pre[i]);
-        for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
-            s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
+        if (ZRT_OCCX8) {
+            const unsigned long long* m64 = reinterpret_cast<const unsigned long long*>(w.occx + w.occx_moff);
+            uint8_t* m8 = reinterpret_cast<uint8_t*>(s_dyn + 2 * w.occx_nbw);
+            for (uint32_t i = threadIdx.x; i < (w.occx_words - w.occx_moff) / 2; i += blockDim.x)
+                m8[i] = (uint8_t)occx_sub8(m64[i]);
+        } else {
+            for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
+                s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
+        }
     }
     __syncthreads();
     OccX L;
     L.ent = reinterpret_cast<const uint2*>(s_dyn);
     L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + 2 * w.occx_nbw);
+    L.masks8 = reinterpret_cast<const uint8_t*>(s_dyn + 2 * w.occx_nbw);
     ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + w.occx_ldsw)[threadIdx.x >> 6];
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1100,11 +1133,20 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             }
         }
         // ---- walk until test_min lanes are parked or nobody walks
+        bool newpark = ZRT_OCCX8 != 0;            // (the refill round may have parked lanes)
         for (;;) {
+            if (ZRT_OCCX8 && newpark) {
+                // a park in an occupied sub-brick may be in an empty cell: its
+                // range has landed by now (a trip later); an empty one walks on
+                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
+                if (st == kPark && rng_slot[lane] == rng_slot[64 + lane]) st = kWalk;
+                newpark = false;
+            }
             const uint64_t wk = __ballot(st == kWalk);
             if (wk == 0ull || (uint32_t)__popcll(__ballot(st == kPark)) >= test_min) break;
             PARK_COUNT(3, 1);
             PARK_COUNT(4, __popcll(wk));
+            uint32_t pk_now = 0;
             if (st == kWalk) {
                 // ZRT_WALK_STEPS DDA steps per trip, every cell's lookup in
                 // flight before any is used; the trip ends in the first cell
@@ -1151,7 +1193,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 st = lm_selu(dn, kDone, st);
                 s = sel;
-                if (lm_selu(pkd, 1u, 0u)) {
+                pk_now = lm_selu(pkd, 1u, 0u);
+                if (pk_now) {
                     const uint32_t x = s.pc ^ prev;
                     const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
                                                       : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
@@ -1159,6 +1202,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     st = kPark;
                 }
             }
+            if (ZRT_OCCX8) newpark = __ballot(pk_now != 0u) != 0ull;
         }
         PARK_STAMP(1);
         // ---- test round: the parked lanes' cells, all pairs over all lanes
@@ -1920,6 +1964,7 @@ static void occx_layout(uint64_t nbw, uint64_t occupied, uint64_t* moff, uint64_
 }
 // u32 words of the LDS copy: 8-byte (bits, prefix) entries, then the masks
 static uint64_t occx_lds_words(uint64_t nbw, uint64_t moff, uint64_t words) {
+    if (ZRT_OCCX8) return (2 * nbw + ((words - moff) / 2 + 3) / 4 + 3) & ~3ull;   // one byte per mask
     return (2 * nbw + (words - moff) + 3) & ~3ull;
 }
 
@@ -2427,7 +2472,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
     int park_block = kParkBlock;
-#ifdef ZRT_SWEEP
+#if defined(ZRT_SWEEP) || ZRT_OCCX8
     if (const char* e = getenv("ZRT_PARK_BLOCK")) park_block = std::max(64, std::min(kParkBlock, atoi(e) / 64 * 64));
 #endif
     const uint32_t occx_ldsw = (uint32_t)occx_lds_words(c->occx_nbw, c->occx_moff, c->occx_words);
