@@ -330,9 +330,12 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
 // runs the same bilinear arithmetic on it (bit-identical: x - x is not
 // folded, NaN/inf weights propagate as before), instead of the index
 // arithmetic and four loads per channel.
+#ifndef ZRT_TEX1
+#define ZRT_TEX1 1
+#endif
 __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, float u, float v) {
     const float* b = texels + t.off;
-    if (t.w == 1 && t.h == 1) {
+    if (ZRT_TEX1 && t.w == 1 && t.h == 1) {
         const float fu = tex_frac(u), fv = tex_frac(v);
         const float x = b[0], y = b[1], z = b[2];
         return mk(bilerp(x, x, x, x, fu, fv), bilerp(y, y, y, y, fu, fv), bilerp(z, z, z, z, fu, fv));
@@ -346,7 +349,7 @@ __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, floa
 }
 __device__ __forceinline__ float sample1(const float* texels, const DevTex& t, float u, float v) {
     const float* b = texels + t.off;
-    if (t.w == 1 && t.h == 1) {                           // the 1x1 dummy (see sample3)
+    if (ZRT_TEX1 && t.w == 1 && t.h == 1) {               // the 1x1 dummy (see sample3)
         const float x = b[0];
         return bilerp(x, x, x, x, tex_frac(u), tex_frac(v));
     }
@@ -579,10 +582,14 @@ __device__ __forceinline__ uint32_t origin_bin(const WfParams& w, v3 no) {
 // `sp` (ZRT_SWEEP builds, the shade kernel only): per-wave s_memtime cycles
 // and active lanes of the phases (SHADE_STAMP), else null.
 #ifdef ZRT_SWEEP
-// phase k: cycles into sp[k], active lanes into sp[8 + k]; sp[16] the last tick.
-// `v`: a value the phase produced, so the stamp waits for it
+// phase k: cycles into sp[k], active lanes into sp[8 + k]; sp[16] the last
+// tick.  `sp` is the wave's row in LDS, updated by the first active lane, so
+// a stamp inside a divergent branch (the hit path) counts for the wave
+// whichever lanes run it.  `v`: a value the phase produced, so the stamp
+// waits for it.
 #define SHADE_STAMP(k, v) do { if (sp) { asm volatile("" :: "v"(v)); const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-    sp[k] += t_ - sp[16]; sp[16] = t_; sp[8 + (k)] += (uint64_t)__popcll(__ballot(1)); } } while (0)
+    const uint32_t n_ = (uint32_t)__popcll(__ballot(1)); \
+    if (first_active_lane()) { sp[k] += t_ - sp[16]; sp[16] = t_; sp[8 + (k)] += n_; } } } while (0)
 #else
 #define SHADE_STAMP(k, v) do { (void)sp; } while (0)
 #endif
@@ -1346,9 +1353,11 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
 #ifdef ZRT_SWEEP
     // ZRT_SWEEP builds: per-wave cycles and active lanes of the shading phases
     // (SHADE_STAMP; printed as zrt_shade_profile with ZRT_PARK_PROFILE)
-    unsigned long long sprof[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    sprof[16] = __builtin_amdgcn_s_memtime();
-    unsigned long long* const sp = sprof;
+    __shared__ unsigned long long s_sprof[kTraceBlock / 64][17];
+    unsigned long long* const sp = s_sprof[threadIdx.x >> 6];
+    if (lane < 16) sp[lane] = 0;
+    if (lane == 16) sp[16] = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_wave_barrier();
 #else
     unsigned long long* const sp = nullptr;
 #endif
@@ -1379,7 +1388,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
     if (lane == 0) atomicAdd(&p.stats[0], s0);
 #ifdef ZRT_SWEEP
     if (lane == 0)
-        for (int k = 0; k < 16; ++k) atomicAdd(&p.stats[32 + k], sprof[k]);
+        for (int k = 0; k < 16; ++k) atomicAdd(&p.stats[32 + k], sp[k]);
 #endif
 }
 

@@ -149,16 +149,17 @@ def lib():
     L.zrt_context_profile.argtypes = [C.c_void_p, C.POINTER(KernelProfile)]
     L.zrt_context_destroy.argtypes = [C.c_void_p]
     L.zrt_context_destroy.restype = None
-    L.zrt_group_create.argtypes = [C.POINTER(Scene), C.POINTER(C.c_int32), C.c_uint32, C.POINTER(C.c_void_p)]
-    L.zrt_group_create_built.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
-                                         C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(Material),
-                                         C.POINTER(C.c_float), C.c_uint64, C.POINTER(C.c_int32), C.c_uint32,
-                                         C.POINTER(C.c_void_p)]
-    L.zrt_group_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig), C.c_void_p,
-                                   C.POINTER(Stats)]
-    L.zrt_group_context.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
-    L.zrt_group_destroy.argtypes = [C.c_void_p]
-    L.zrt_group_destroy.restype = None
+    if hasattr(L, "zrt_group_create"):      # ABI 2 (an ABI-1 build: tools/ A/B baselines only)
+        L.zrt_group_create.argtypes = [C.POINTER(Scene), C.POINTER(C.c_int32), C.c_uint32, C.POINTER(C.c_void_p)]
+        L.zrt_group_create_built.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(Material),
+                                             C.POINTER(C.c_float), C.c_uint64, C.POINTER(C.c_int32), C.c_uint32,
+                                             C.POINTER(C.c_void_p)]
+        L.zrt_group_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.POINTER(RenderConfig), C.c_void_p,
+                                       C.POINTER(Stats)]
+        L.zrt_group_context.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
+        L.zrt_group_destroy.argtypes = [C.c_void_p]
+        L.zrt_group_destroy.restype = None
     L.zrt_tile_pixels.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_void_p, C.POINTER(C.c_uint32)]
     L.zrt_camera_from_matrix.argtypes = [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int32,
