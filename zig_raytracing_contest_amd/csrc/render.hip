@@ -76,17 +76,17 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
-// ZRT_OCCX8: the park kernel's LDS OccX holds an 8-bit mask of occupied 2^3
-// sub-bricks per occupied 4^3 brick instead of the 64-bit cell mask (~47 KB
-// less LDS on the contest stand-in); a lane then parks in any cell of an
-// occupied sub-brick and an empty range unparks it at the next trip
-// (measured variant, off)
-#ifndef ZRT_OCCX8
-#define ZRT_OCCX8 0
+// ZRT_PARK_MISS: a bounce segment that misses ends in the park kernel
+// (terminal radiance = the sky colour, stage3.zig:195-197), so the shade
+// kernel loads the path records of hits only
+#ifndef ZRT_PARK_MISS
+#define ZRT_PARK_MISS 0
 #endif
-// ZRT_SPATIAL: bounce queues binned by origin octant (measured variant, off)
-#ifndef ZRT_SPATIAL
-#define ZRT_SPATIAL 0
+// ZRT_SHADE_PACK (with ZRT_PARK_MISS): the shade kernel packs the hit entries
+// of its fetches densely over the wave (an LDS list per wave) before shading,
+// so every lane of a shading step holds a hit
+#ifndef ZRT_SHADE_PACK
+#define ZRT_SHADE_PACK 0
 #endif
 // DDA steps per park walk trip, every cell's brick lookup in flight at once
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
@@ -196,10 +196,6 @@ __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uin
 // and masks.)
 __device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
     const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
-    if (ZRT_OCCX8) {   // sub-brick ((x >> 1) & 1) | ((y >> 1) & 1) << 1 | ((z >> 1) & 1) << 2
-        const uint32_t sb = ((i >> 1) & 1u) | ((i >> 2) & 2u) | ((i >> 3) & 4u);
-        return ((uint32_t)bm >> sb) & 1u;
-    }
     return (uint32_t)(bm >> (i & 63u)) & 1u;
 }
 
@@ -538,15 +534,6 @@ struct WfParams {
     uint32_t occx_ldsw;       // u32 words OccX takes in LDS (multiple of 4): entries + masks
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
-    // ZRT_SPATIAL (measured variant): bounce queues binned by
-    // the octant of the next segment's origin around spl[] instead of by pixel
-    // range; region g of a binned queue starts at the prefix of the per-octant
-    // counts the launch's park kernel histogrammed (hist), so it needs no
-    // per-region capacity
-    uint32_t spatial_in, spatial_out;     // q_in / q_out binned by octant
-    const uint32_t* hist_in;              // counts per region of q_in (binned)
-    uint32_t* hist_out;                   // park kernel: counts per region the shade kernel appends
-    float spl[3];
 };
 
 // Work / append counters: one per 128-byte line (32 u32), so the waves'
@@ -560,18 +547,8 @@ __device__ __forceinline__ uint32_t xcd_q0(uint32_t P, uint32_t g) {
     return min(P, (nblk * g / 8u) * 64u);
 }
 
-// First queue entry of region g: pixel-range regions at S * (first pixel),
-// octant-binned ones at the prefix of the launch's per-region counts.
-__device__ __forceinline__ uint32_t region_base(const WfParams& w, uint32_t binned, const uint32_t* hist, uint32_t g) {
-    if (!ZRT_SPATIAL || !binned) return w.t.S * xcd_q0(w.t.P, g);
-    uint32_t b = 0;
-    for (uint32_t h = 0; h < g; ++h) b += hist[h * kCtr];
-    return b;
-}
-// The octant (region) of a next-segment origin.
-__device__ __forceinline__ uint32_t origin_bin(const WfParams& w, v3 no) {
-    return (no.x >= w.spl[0] ? 1u : 0u) | (no.y >= w.spl[1] ? 2u : 0u) | (no.z >= w.spl[2] ? 4u : 0u);
-}
+// First queue entry of region g: S * (the first pixel of pixel range g).
+__device__ __forceinline__ uint32_t region_base(const WfParams& w, uint32_t g) { return w.t.S * xcd_q0(w.t.P, g); }
 
 // traceRayRecursive's body after the hit (stage3.zig:195-219) for one
 // segment: env colour on a miss, else material lookup, (e, a) pair to the
@@ -647,9 +624,8 @@ __device__ __forceinline__ void q_store(const WfParams& w, uint32_t pos, v3 o, v
 }
 
 // Append the continuing paths of the wave (lanes with `cont`) to the next
-// queue, each to the region `reg` (its pixel range; ZRT_SPATIAL: its origin's
-// octant): one returning atomic per distinct region of the wave, ranks from
-// ballot + popcount.
+// queue, each to the region `reg` of its pixel range: one returning atomic
+// per distinct region of the wave, ranks from ballot + popcount.
 __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t below, v3 o, v3 d, uint32_t item,
                                           uint32_t depth, uint32_t slot, const Rng& rng, uint32_t mask,
                                           uint32_t reg) {
@@ -660,7 +636,7 @@ __device__ __forceinline__ void wf_append(const WfParams& w, bool cont, uint64_t
         const uint64_t m = __ballot(cont && reg == g);
         uint32_t ob = 0;
         if ((threadIdx.x & 63u) == lead) ob = atomicAdd(&w.n_out8[g * kCtr], (uint32_t)__popcll(m));
-        ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)lead) + region_base(w, w.spatial_out, w.hist_out, g);
+        ob = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)lead) + region_base(w, g);
         if (cont && reg == g) q_store(w, ob + (uint32_t)__popcll(m & below), o, d, item, depth, slot, rng, mask);
         pend &= ~m;
     }
@@ -703,8 +679,7 @@ __device__ __forceinline__ bool wf_fetch(const WfParams& w, uint32_t want, uint3
 // Bounce launches: entry j of region g is queue index S * q0 + j.
 template <bool PRIMARY>
 __device__ __forceinline__ uint32_t ent_index(const WfParams& w, uint32_t grp, uint32_t j) {
-    if (PRIMARY) return w.t.S * xcd_q0(w.t.P, grp) + j;
-    return region_base(w, w.spatial_in, w.hist_in, grp) + j;
+    return region_base(w, grp) + j;
 }
 
 // The path state of queue entry / primary item `i` that shading needs.
@@ -852,25 +827,13 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
 struct OccX {
     const uint2* ent;                    // (brick bits, 1 + occupied bricks before the word)
     const unsigned long long* masks;     // [0]: zero mask
-    const uint8_t* masks8;               // ZRT_OCCX8: sub-brick masks, [0] zero
 };
 __device__ __forceinline__ unsigned long long occx_mask_at(const OccX& L, uint2 e, uint32_t b) {
     const uint32_t low = __builtin_amdgcn_ubfe(e.x, 0u, b);        // bits of the bricks below b
     const uint32_t bit = __builtin_amdgcn_ubfe(e.x, b, 1u);
-    if (ZRT_OCCX8) return L.masks8[__umul24((uint32_t)__popc(low) + e.y, bit)];
     return L.masks[__umul24((uint32_t)__popc(low) + e.y, bit)];
 }
-// a 64-bit cell mask -> its 8-bit sub-brick mask (ZRT_OCCX8)
-__device__ __forceinline__ uint32_t occx_sub8(unsigned long long m) {
-    uint32_t r = 0;
-    for (uint32_t sb = 0; sb < 8; ++sb) {
-        const uint32_t x = (sb & 1u) << 1, y = sb & 2u, z = (sb >> 1) & 2u;   // sub-brick origin cell
-        const uint32_t i0 = x | (y << 2) | (z << 4);
-        const unsigned long long sub = (3ull << i0) | (3ull << (i0 + 4)) | (3ull << (i0 + 16)) | (3ull << (i0 + 20));
-        r |= (m & sub) ? (1u << sb) : 0u;
-    }
-    return r;
-}
+
 __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t b) {
     return occx_mask_at(L, L.ent[b >> 5], b);
 }
@@ -1009,21 +972,13 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
         const uint16_t* pre = reinterpret_cast<const uint16_t*>(w.occx + w.occx_nbw);
         uint2* ent = reinterpret_cast<uint2*>(s_dyn);
         for (uint32_t i = threadIdx.x; i < w.occx_nbw; i += blockDim.x) ent[i] = make_uint2(w.occx[i], pre[i]);
-        if (ZRT_OCCX8) {
-            const unsigned long long* m64 = reinterpret_cast<const unsigned long long*>(w.occx + w.occx_moff);
-            uint8_t* m8 = reinterpret_cast<uint8_t*>(s_dyn + 2 * w.occx_nbw);
-            for (uint32_t i = threadIdx.x; i < (w.occx_words - w.occx_moff) / 2; i += blockDim.x)
-                m8[i] = (uint8_t)occx_sub8(m64[i]);
-        } else {
-            for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
-                s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
-        }
+        for (uint32_t i = threadIdx.x; i < w.occx_words - w.occx_moff; i += blockDim.x)
+            s_dyn[2 * w.occx_nbw + i] = w.occx[w.occx_moff + i];
     }
     __syncthreads();
     OccX L;
     L.ent = reinterpret_cast<const uint2*>(s_dyn);
     L.masks = reinterpret_cast<const unsigned long long*>(s_dyn + 2 * w.occx_nbw);
-    L.masks8 = reinterpret_cast<const uint8_t*>(s_dyn + 2 * w.occx_nbw);
     ParkSlot& W = reinterpret_cast<ParkSlot*>(s_dyn + w.occx_ldsw)[threadIdx.x >> 6];
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1045,7 +1000,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
-    uint32_t pdepth = 0;                   // its depth (ZRT_SPATIAL's histogram)
+    uint32_t pitem = 0, pmask = 0;         // ZRT_PARK_MISS: its item and scatter mask
     PARK_PROF_DECL
 
     for (;;) {
@@ -1063,21 +1018,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 const bool done = st == kDone;
                 if (done) {
                     w.hit[qi] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
-                    st = kIdle;
-                }
-                if (ZRT_SPATIAL && w.spatial_out) {            // octant histogram of the paths the
-                    // shade kernel will append: hits with depth left, binned by
-                    // the origin it will compute (the same f32 arithmetic)
-                    const bool app = done && nearest != kInf && pdepth > 1u;
-                    const uint32_t bin = origin_bin(w, add(o, scale(d, nearest + kFltEps)));
-                    uint64_t pend = __ballot(app);
-                    while (pend) {
-                        const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
-                        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
-                        const uint64_t m = __ballot(app && bin == g);
-                        if (lane == lead) atomicAdd(&w.hist_out[g * kCtr], (uint32_t)__popcll(m));
-                        pend &= ~m;
+                    if (ZRT_PARK_MISS && nearest == kInf) {   // stage3.zig:195-197: the sky ends the path
+                        const v3 L = env_color(d);
+                        w.term[pitem] = make_float4(L.x, L.y, L.z, __uint_as_float(pmask));
                     }
+                    st = kIdle;
                 }
                 __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
             }
@@ -1105,7 +1050,10 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
                             o = mk(qa.x, qa.y, qa.z);
                             d = mk(qb.x, qb.y, qb.z);
-                            pdepth = __float_as_uint(qb.w) & 0xFFFFu;
+                            if (ZRT_PARK_MISS) {
+                                pitem = __float_as_uint(qa.w);
+                                pmask = reinterpret_cast<const uint32_t*>(w.q_in + 3ull * qi + 2)[2];
+                            }
                         }
                         {                                          // queued paths have depth >= 1
                             nearest = kInf;
@@ -1140,20 +1088,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             }
         }
         // ---- walk until test_min lanes are parked or nobody walks
-        bool newpark = ZRT_OCCX8 != 0;            // (the refill round may have parked lanes)
         for (;;) {
-            if (ZRT_OCCX8 && newpark) {
-                // a park in an occupied sub-brick may be in an empty cell: its
-                // range has landed by now (a trip later); an empty one walks on
-                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
-                if (st == kPark && rng_slot[lane] == rng_slot[64 + lane]) st = kWalk;
-                newpark = false;
-            }
             const uint64_t wk = __ballot(st == kWalk);
             if (wk == 0ull || (uint32_t)__popcll(__ballot(st == kPark)) >= test_min) break;
             PARK_COUNT(3, 1);
             PARK_COUNT(4, __popcll(wk));
-            uint32_t pk_now = 0;
             if (st == kWalk) {
                 // ZRT_WALK_STEPS DDA steps per trip, every cell's lookup in
                 // flight before any is used; the trip ends in the first cell
@@ -1200,8 +1139,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 st = lm_selu(dn, kDone, st);
                 s = sel;
-                pk_now = lm_selu(pkd, 1u, 0u);
-                if (pk_now) {
+                if (lm_selu(pkd, 1u, 0u)) {
                     const uint32_t x = s.pc ^ prev;
                     const uint32_t face = (x & pk.f0) ? (s.d0 >> 31)
                                                       : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
@@ -1209,7 +1147,6 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     st = kPark;
                 }
             }
-            if (ZRT_OCCX8) newpark = __ballot(pk_now != 0u) != 0ull;
         }
         PARK_STAMP(1);
         // ---- test round: the parked lanes' cells, all pairs over all lanes
@@ -1304,7 +1241,7 @@ __device__ __forceinline__ void shade_path(const WfParams& w, const double* zx, 
         if (!cont) w.term[item] = make_float4(L.x, L.y, L.z, __uint_as_float(mask));
     }
     SHADE_STAMP(6, o.x);                       // the rest of the segment (misses, pass-through, terminal store)
-    wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, ZRT_SPATIAL && w.spatial_out ? origin_bin(w, o) : grp);
+    wf_append(w, cont, below, o, d, item, depth, slot, rng, mask, grp);
     SHADE_STAMP(7, o.x);                       // append
 }
 
@@ -1365,24 +1302,113 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
     // loaded before the first is shaded, so their latency overlaps the
     // earlier entries' dependent chains (2: cfg3 +1.2%, cfg2 / cfg5 within
     // noise, 112 VGPRs, r02c6)
+    if (ZRT_SHADE_PACK && ZRT_PARK_MISS) {
+        // the wave's hit entries (queue index, region), packed in fetch order
+        constexpr uint32_t kCap = 128u * kShadeEntries;
+        __shared__ uint32_t s_hq[kTraceThreads / 64][kCap];   // launched with kTraceThreads
+        __shared__ uint8_t s_hg[kTraceThreads / 64][kCap];
+        uint32_t* const hq = s_hq[threadIdx.x >> 6];
+        uint8_t* const hg = s_hg[threadIdx.x >> 6];
+        uint32_t nbuf = 0;                     // wave-uniform
+        for (;;) {
+            uint32_t base = 0, lim = 0;
+            const bool got = wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim);
+            SHADE_STAMP(0, base);
+            if (got) {
+#pragma unroll
+                for (int e = 0; e < kShadeEntries; ++e) {
+                    const uint32_t j = base + 64u * e + lane;
+                    const uint32_t i = j < lim ? ent_index<false>(w, grp, j) : 0u;
+                    const float t = j < lim ? w.hit[i].x : kInf;
+                    const bool hit = t != kInf;
+                    n_seg += (j < lim && !hit) ? 1u : 0u;      // the misses' segments (ended by the park kernel)
+                    const uint64_t hm = __ballot(hit);
+                    if (hit) {
+                        const uint32_t pos = nbuf + (uint32_t)__popcll(hm & below);
+                        hq[pos] = i;
+                        hg[pos] = (uint8_t)grp;
+                    }
+                    nbuf += (uint32_t)__popcll(hm);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            while (nbuf >= 64u * kShadeEntries || (!got && nbuf > 0u)) {
+                const uint32_t n = min(nbuf, 64u * kShadeEntries);
+                float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
+                uint32_t g[kShadeEntries];
+                bool ok[kShadeEntries];
+#pragma unroll
+                for (int e = 0; e < kShadeEntries; ++e) {
+                    const uint32_t k = 64u * e + lane;
+                    ok[e] = k < n;
+                    const uint32_t i = ok[e] ? hq[k] : 0u;
+                    g[e] = ok[e] ? hg[k] : 0u;
+                    a[e] = b[e] = c[e] = h[e] = z4;
+                    if (ok[e]) {
+                        h[e] = w.hit[i];
+                        a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // the rest moves to the front (fewer than kCap - n entries)
+                for (uint32_t k = lane; k + n < nbuf; k += 64u) {
+                    const uint32_t q = hq[k + n];
+                    const uint8_t gg = hg[k + n];
+                    __builtin_amdgcn_wave_barrier();
+                    hq[k] = q;
+                    hg[k] = gg;
+                }
+                __builtin_amdgcn_wave_barrier();
+                nbuf -= n;
+#pragma unroll
+                for (int e = 0; e < kShadeEntries; ++e)
+                    shade_entry(w, zx, zf, mats, ok[e], a[e], b[e], c[e], h[e], below, g[e], n_seg, sp);
+            }
+            if (!got) break;
+        }
+    } else
     for (;;) {
         uint32_t base = 0, lim = 0;
         if (!wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim)) break;
         SHADE_STAMP(0, base);                  // work atomic
         float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
+        bool hit[kShadeEntries];
+        if (ZRT_PARK_MISS) {
+            // the park kernel ended the misses: hit records first, then the
+            // path records of the hits (loaded beside their triangle data)
+            uint32_t ie[kShadeEntries];
 #pragma unroll
-        for (int e = 0; e < kShadeEntries; ++e) {
-            const uint32_t j = base + 64u * e + lane;
-            a[e] = b[e] = c[e] = h[e] = z4;
-            if (j < lim) {
-                const uint32_t i = ent_index<false>(w, grp, j);
-                a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2]; h[e] = w.hit[i];
+            for (int e = 0; e < kShadeEntries; ++e) {
+                const uint32_t j = base + 64u * e + lane;
+                ie[e] = j < lim ? ent_index<false>(w, grp, j) : 0u;
+                h[e] = j < lim ? w.hit[ie[e]] : make_float4(kInf, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int e = 0; e < kShadeEntries; ++e) {
+                const uint32_t j = base + 64u * e + lane;
+                hit[e] = j < lim && h[e].x != kInf;
+                n_seg += (j < lim && !hit[e]) ? 1u : 0u;      // the misses' segments
+                a[e] = b[e] = c[e] = z4;
+                if (hit[e]) {
+                    const uint32_t i = ie[e];
+                    a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < kShadeEntries; ++e) {
+                const uint32_t j = base + 64u * e + lane;
+                a[e] = b[e] = c[e] = h[e] = z4;
+                hit[e] = j < lim;
+                if (j < lim) {
+                    const uint32_t i = ent_index<false>(w, grp, j);
+                    a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2]; h[e] = w.hit[i];
+                }
             }
         }
 #pragma unroll
         for (int e = 0; e < kShadeEntries; ++e)
-            shade_entry(w, zx, zf, mats, base + 64u * e + lane < lim, a[e], b[e], c[e], h[e], below, grp, n_seg,
-                        sp);
+            shade_entry(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e], below, grp, n_seg, sp);
     }
     const unsigned long long s0 = wave_sum(n_seg);
     if (lane == 0) atomicAdd(&p.stats[0], s0);
@@ -1587,7 +1613,6 @@ struct zrt_context {
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
-    float spl[3] = {0.0f, 0.0f, 0.0f};  // ZRT_SPATIAL: octant split point (median ref v0)
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;     // counting build
@@ -1925,14 +1950,6 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
     HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
-    if (ZRT_SPATIAL && c->nrefs) {             // octant split: the refs' median v0 per axis
-        std::vector<float> v(c->nrefs);
-        for (int a = 0; a < 3; ++a) {
-            for (uint32_t i = 0; i < c->nrefs; ++i) v[i] = s->triangles_pos[9ull * i + a];
-            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-            c->spl[a] = v[v.size() / 2];
-        }
-    }
     if ((rc = context_materials(c, s)) != ZRT_OK) return rc;
     return context_occupancy(c, s->cells);
 }
@@ -1973,7 +1990,6 @@ static void occx_layout(uint64_t nbw, uint64_t occupied, uint64_t* moff, uint64_
 }
 // u32 words of the LDS copy: 8-byte (bits, prefix) entries, then the masks
 static uint64_t occx_lds_words(uint64_t nbw, uint64_t moff, uint64_t words) {
-    if (ZRT_OCCX8) return (2 * nbw + ((words - moff) / 2 + 3) / 4 + 3) & ~3ull;   // one byte per mask
     return (2 * nbw + (words - moff) + 3) & ~3ull;
 }
 
@@ -2438,7 +2454,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     const bool packed = c->packed;
-    const bool spatial = ZRT_SPATIAL && park_next;   // binned queues need the park kernel's histogram
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
     const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
@@ -2481,7 +2496,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // occupancy-sized persistent grids
     const size_t lds_wf = 4ull * c->occ_words;
     int park_block = kParkBlock;
-#if defined(ZRT_SWEEP) || ZRT_OCCX8
+#ifdef ZRT_SWEEP
     if (const char* e = getenv("ZRT_PARK_BLOCK")) park_block = std::max(64, std::min(kParkBlock, atoi(e) / 64 * 64));
 #endif
     const uint32_t occx_ldsw = (uint32_t)occx_lds_words(c->occx_nbw, c->occx_moff, c->occx_words);
@@ -2630,13 +2645,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 W.n_out8 = wfc + kCtr * (16 * (k + 1) + 8);
                 W.hit = hit;
                 W.fetch8s = wfc + kCtr * (16 * (mb + 2) + 8 * k);
-                // ZRT_SPATIAL: the shade half of launch k >= 1 appends by octant
-                // (histogrammed by its park half); launch k + 1 reads those regions
-                W.spatial_out = spatial && k >= 1;
-                W.spatial_in = spatial && k >= 2;
-                W.hist_out = wfc + kCtr * (24 * (mb + 2) + 8 * k);
-                W.hist_in = k ? wfc + kCtr * (24 * (mb + 2) + 8 * (k - 1)) : nullptr;
-                for (int a = 0; a < 3; ++a) W.spl[a] = c->spl[a];
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 const int cls = k == 0 ? ZRT_KERNEL_PRIMARY : (park_next ? ZRT_KERNEL_PARK : ZRT_KERNEL_BOUNCE);
                 if ((rc = kt_begin(cls, sm)) != ZRT_OK) return rc;
