@@ -151,6 +151,61 @@ static std::vector<Rec> walk_skip(const TestGrid& g, const GridK& k, Dda s, uint
     return out;
 }
 
+// BRICK_SKIPV (the primary lane walk's skip on the packed state) with
+// DDAV_STEPX in occupied bricks: the same cells of occupied bricks with the
+// same crossing ts as the cell walk, each skip's TC the exit t of the last
+// cell the cell walk passes in that brick, EXITED exactly at the grid exit
+static uint64_t g_skipv_fails = 0, g_skipv = 0;
+static void walk_skipv(const TestGrid& g, const GridK& k, const Dda& s0, const std::vector<Rec>& ref) {
+    const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
+    PackK pk;
+    if (!pack_layout(res, pk)) return;
+    DdaV x;
+    ddav_from(s0, k, pk, x);
+    Dda q = s0;                                   // the cell walk alongside
+    size_t n = 0;
+    for (int guard = 0; guard < 100000; ++guard) {
+        const uint32_t c0 = x.pc & pk.f0, c1 = (x.pc & pk.f1) >> pk.o1, c2 = (x.pc & pk.f2) >> pk.o2;
+        const bool occ = g.occupied(c0, c1, c2);
+        if (occ) {
+            if (n >= ref.size() || ref[n].c0 != c0 || ref[n].c1 != c1 || ref[n].c2 != c2 ||
+                memcmp(&ref[n].tn0, &x.tn0, 4) || memcmp(&ref[n].tn1, &x.tn1, 4) || memcmp(&ref[n].tn2, &x.tn2, 4)) {
+                ++g_skipv_fails;
+                return;
+            }
+            ++n;
+        }
+        bool exited, crossed;
+        float tc;
+        if (!occ && s0.neg < 8u) {
+            float last = 0.0f;
+            for (;;) {                                // the cell walk to the brick's last cell
+                bool cr;
+                DDA_STEP(q, k, 2, cr, last);
+                if (cr || last == kInf) break;
+            }
+            BRICK_SKIPV(x, pk, exited, tc);
+            ++g_skipv;
+            const float te = exited ? kInf : tc;
+            if (memcmp(&te, &last, 4) != 0) { ++g_skipv_fails; return; }
+        } else {
+            float last;
+            bool cr;
+            DDA_STEP(q, k, 2, cr, last);
+            DDAV_STEPX(x, pk, pk.low2, crossed, exited, tc);
+            const float te = exited ? kInf : tc;
+            if (memcmp(&te, &last, 4) != 0) { ++g_skipv_fails; return; }
+        }
+        if (exited) break;
+        if (x.pc != pack_cellv(pk, q.c0, q.c1, q.c2) || memcmp(&q.tn0, &x.tn0, 4) || memcmp(&q.tn1, &x.tn1, 4) ||
+            memcmp(&q.tn2, &x.tn2, 4)) {
+            ++g_skipv_fails;
+            return;
+        }
+    }
+    if (n != ref.size() && !(ref.size() == n + 1 && ref[n].c0 == ~0u)) ++g_skipv_fails;
+}
+
 int main(int argc, char** argv) {
     const int n_grids = argc > 1 ? atoi(argv[1]) : 40;
     const int n_rays = argc > 2 ? atoi(argv[2]) : 4000;
@@ -201,6 +256,7 @@ int main(int argc, char** argv) {
             walk_w(k, s);
             const auto a = walk_cells(g, k, s);
             const auto b = walk_skip(g, k, s, &skips);
+            walk_skipv(g, k, s, a);
             if (!(a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin()))) {
                 if (++fails <= 5)
                     fprintf(stderr, "MISMATCH grid %d ray %d: %zu vs %zu cells (o=%g,%g,%g d=%g,%g,%g)\n", gi, r,
@@ -208,11 +264,11 @@ int main(int argc, char** argv) {
             }
         }
     }
-    fails += g_texit_fails + g_walk_fails;
+    fails += g_texit_fails + g_walk_fails + g_skipv_fails;
     printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, "
-           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"fails\": %llu}\n",
+           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"skipv\": %llu, \"skipv_fails\": %llu, \"fails\": %llu}\n",
            (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
            (unsigned long long)g_texit_fails, (unsigned long long)g_walk_steps, (unsigned long long)g_walk_fails,
-           (unsigned long long)fails);
+           (unsigned long long)g_skipv, (unsigned long long)g_skipv_fails, (unsigned long long)fails);
     return fails ? 1 : 0;
 }

@@ -443,6 +443,60 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
         (S).lin = (S).c2 * (G).str2 + (S).c1 * (G).str1 + (S).c0;                             \
     } while (0)
 
+// BRICK_SKIP4 on the packed state (DdaV, PackK): the primary lane walk's
+// empty-brick skip.  Same merge argument: per axis a the cells left inside
+// the 4^3 brick (or to the grid exit, whichever is nearer) m1_a, the
+// brick-exit crossing E_a = T_a(m1_a + 1) from the same f32 adds, the exit
+// axis X = the first E_a in (t, -axis) order, and every other axis takes the
+// crossings T_b(j) that precede E_X in that order (ties to the higher axis,
+// as Iterator.next's booleans); axis X takes m1_X + 1.  The signs come from
+// the packed steps (d_a < 0 as u32 top bit).  Not used with a -inf/NaN
+// crossing sequence (Dda.neg bit 3).  EXITED / TC as DDAV_STEPX: the break
+// test nearest <= T_EXIT of the last skipped cell is EXITED || nearest <= TC
+// (tests/cpp/dda_skip_check.cpp checks it against the cell walk).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ZRT_UBFE(X, O, W) __builtin_amdgcn_ubfe((X), (O), (W))
+#else
+#define ZRT_UBFE(X, O, W) ((W) == 0u ? 0u : (((X) >> (O)) & (0xFFFFFFFFu >> (32u - (W)))))
+#endif
+#define SKIPV_AXIS(S, A, OA, BA)                                                               \
+    const uint32_t c##A##_ = ZRT_UBFE((S).pc, (OA), (BA));                                      \
+    const uint32_t xn##A##_ = (uint32_t)((int32_t)(S).d##A >> 31);                              \
+    const uint32_t rem##A##_ = ~(c##A##_ ^ xn##A##_) & 3u;                                      \
+    const uint32_t te##A##_ = xn##A##_ ? c##A##_ : ZRT_UBFE((S).pe, (OA), (BA)) - c##A##_;      \
+    const uint32_t m1##A##_ = zmin(rem##A##_, te##A##_);                                        \
+    const bool out##A##_ = te##A##_ <= rem##A##_;                                               \
+    const float T##A##1_ = (S).tn##A;                                                           \
+    const float T##A##2_ = T##A##1_ + (S).td##A;                                                \
+    const float T##A##3_ = T##A##2_ + (S).td##A;                                                \
+    const float T##A##4_ = T##A##3_ + (S).td##A;                                                \
+    const float E##A##_ = m1##A##_ == 0u ? T##A##1_                                             \
+                        : (m1##A##_ == 1u ? T##A##2_ : (m1##A##_ == 2u ? T##A##3_ : T##A##4_));
+#define SKIPV_COUNT(S, A, TIE)                                                                 \
+    uint32_t k##A##_ = ((T##A##1_ < ex_ || (T##A##1_ == ex_ && (TIE))) ? 1u : 0u) +             \
+                       ((T##A##2_ < ex_ || (T##A##2_ == ex_ && (TIE))) ? 1u : 0u) +             \
+                       ((T##A##3_ < ex_ || (T##A##3_ == ex_ && (TIE))) ? 1u : 0u);              \
+    k##A##_ = x##A##_ ? m1##A##_ + 1u : k##A##_;                                                \
+    (S).tn##A = k##A##_ == 0u ? T##A##1_                                                        \
+              : (k##A##_ == 1u ? T##A##2_                                                       \
+              : (k##A##_ == 2u ? T##A##3_ : (k##A##_ == 3u ? T##A##4_ : T##A##4_ + (S).td##A)));
+#define BRICK_SKIPV(S, K, EXITED, TC)                                                          \
+    do {                                                                                       \
+        SKIPV_AXIS(S, 0, 0u, (K).b0)                                                           \
+        SKIPV_AXIS(S, 1, (K).o1, (K).b1)                                                       \
+        SKIPV_AXIS(S, 2, (K).o2, (K).b2)                                                       \
+        const bool x0_ = E0_ < E1_ && E0_ < E2_;                                               \
+        const bool x1_ = !(E0_ < E1_) && E1_ < E2_;                                            \
+        const bool x2_ = !x0_ && !x1_;                                                         \
+        const float ex_ = x0_ ? E0_ : (x1_ ? E1_ : E2_);                                       \
+        SKIPV_COUNT(S, 0, false)                                                               \
+        SKIPV_COUNT(S, 1, x0_)                                                                 \
+        SKIPV_COUNT(S, 2, !x2_)                                                                \
+        (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                        \
+        (TC) = ex_;                                                                            \
+        (S).pc += k0_ * (S).d0 + k1_ * (S).d1 + k2_ * (S).d2;                                  \
+    } while (0)
+
 // Select of the park kernel's pair refill (render.hip): position of the r-th
 // (from 0) set bit of m, r < popcount(m).  The byte holding it comes from
 // three prefix popcounts, its position within the byte from a 2 KB LDS table

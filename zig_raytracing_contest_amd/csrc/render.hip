@@ -76,6 +76,12 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
+// ZRT_PRIM_SKIP: the primary lane walk crosses empty 4^3 bricks in one
+// BRICK_SKIPV (dda.h) instead of cell by cell (camera rays: ~84% of their
+// cells lie in empty bricks, ~4 cells per brick entered, tools/walk_sim.cpp)
+#ifndef ZRT_PRIM_SKIP
+#define ZRT_PRIM_SKIP 0
+#endif
 // ZRT_PARK_MISS: a bounce segment that misses ends in the park kernel
 // (terminal radiance = the sky colour, stage3.zig:195-197), so the shade
 // kernel loads the path records of hits only
@@ -270,6 +276,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         uint32_t f0 = p.pk.f0, f1 = p.pk.f1, f2 = p.pk.f2;
         asm("" : "+s"(f0), "+s"(f1), "+s"(f2));
         bool occupied = brick_occupied_v(p, occ, s.pc);
+        const bool skip_ok = ZRT_PRIM_SKIP && s0.neg < 8u;
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
@@ -279,7 +286,14 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             float tc;
             PackK pkl = p.pk;
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
-            DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
+            if (skip_ok && !occupied) {
+                // the cells left in this empty 4^3 brick at once (a 4^3 part
+                // of a larger empty occupancy brick is empty too)
+                BRICK_SKIPV(s, pkl, exited, tc);
+                crossed = true;
+            } else {
+                DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
+            }
             if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
@@ -947,7 +961,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -1137,6 +1151,23 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     pkd = lm_or(lm_andn(pkd, stop[k]), lm_andn(stop[k], dd[k]));
                     dn = lm_or(lm_andn(dn, stop[k]), dd[k]);
                 }
+#ifdef ZRT_SWEEP
+                {   // lane steps taken (up to the stopping one), those into cells of
+                    // empty bricks, and those that entered an empty brick
+                    LaneM alive = lm_of(true);
+                    uint32_t pcp = s.pc;
+#pragma unroll
+                    for (int k = 0; k < kS; ++k) {
+                        const LaneM emp = lm_of(q[k] == 0ull);
+                        const LaneM ent = lm_of(((pcp ^ ss[k].pc) & ~pk.low2) != 0u);
+                        PARK_COUNT(13, __popcll(alive));
+                        PARK_COUNT(14, __popcll(lm_and(alive, emp)));
+                        PARK_COUNT(15, __popcll(lm_and(lm_and(alive, emp), ent)));
+                        alive = lm_andn(alive, stop[k]);
+                        pcp = ss[k].pc;
+                    }
+                }
+#endif
                 st = lm_selu(dn, kDone, st);
                 s = sel;
                 if (lm_selu(pkd, 1u, 0u)) {
@@ -1217,6 +1248,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
 #ifdef ZRT_SWEEP
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
+    if (lane == 0)
+        for (int k = 13; k < 16; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
 #endif
 }
 
@@ -2719,6 +2752,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 "\"pairs\": %llu, \"refill_rounds\": %llu, \"shaded_lanes\": %llu, \"cyc_drain\": %llu, "
                 "\"cyc_atomic\": %llu, \"cyc_setup\": %llu}}\n",
                 hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
+    if (getenv("ZRT_PARK_PROFILE") && park_next)
+        fprintf(stderr, "{\"zrt_walk_steps\": {\"lane_steps\": %llu, \"empty_brick_steps\": %llu, "
+                "\"empty_brick_entries\": %llu}}\n", hs[48], hs[49], hs[50]);
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);
