@@ -125,6 +125,9 @@ typedef struct zrt_render_config {
                                         (the roofline measurement); same image */
 #define ZRT_FLAG_KERNEL_TIMES 0x20u  /* HIP events around every kernel launch: per-kernel device times
                                         in zrt_context_profile (adds ~10 us per launch) */
+#define ZRT_FLAG_ESCAPE       0x40u  /* the park walk always uses the escape table (by default only on
+                                        scenes where enough of it is set to pay); same image */
+#define ZRT_FLAG_NO_ESCAPE    0x80u  /* the park walk never uses the escape table; same image */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */

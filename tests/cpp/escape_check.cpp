@@ -1,0 +1,128 @@
+// Host check of the escape table (csrc/escape.h): on random grids
+// (anisotropic cells, clustered occupancy so that many bits are set) and
+// random rays, every cell the cell-by-cell walk (DDA_STEP, Iterator.next)
+// visits after a cell whose brick has the ray's escape bit set must be
+// empty.  Also checks the summed-area box query against a direct count.
+//   g++ -O2 -std=c++17 -ffp-contract=off -I<csrc> escape_check.cpp
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "dda.h"
+#include "escape.h"
+
+using namespace zrt;
+
+int main(int argc, char** argv) {
+    const int n_grids = argc > 1 ? atoi(argv[1]) : 24;
+    const int n_rays = argc > 2 ? atoi(argv[2]) : 20000;
+    std::mt19937_64 rng(777);
+    std::uniform_real_distribution<float> U(0.0f, 1.0f);
+    uint64_t rays = 0, escapes = 0, saved = 0, steps = 0, unsound = 0, box_fails = 0, bits_set = 0, bits = 0;
+    for (int gi = 0; gi < n_grids; ++gi) {
+        uint32_t res[3];
+        float bmin[3], bmax[3], cs[3];
+        for (int a = 0; a < 3; ++a) {
+            res[a] = gi == 0 ? 64u : 4u + (uint32_t)(rng() % 60);
+            bmin[a] = -5.0f + 10.0f * U(rng);
+            cs[a] = 0.02f + U(rng);
+            bmax[a] = bmin[a] + cs[a] * (float)res[a];
+        }
+        // occupancy: a few random blobs and planes
+        std::vector<uint8_t> occ((size_t)res[0] * res[1] * res[2], 0);
+        const int nblob = 1 + (int)(rng() % 6);
+        for (int k = 0; k < nblob; ++k) {
+            uint32_t c[3], r[3];
+            for (int a = 0; a < 3; ++a) { c[a] = rng() % res[a]; r[a] = 1 + rng() % (res[a] / 4 + 1); }
+            const bool plane = rng() % 3 == 0;
+            if (plane) r[rng() % 3] = 0;
+            for (uint32_t z = c[2] > r[2] ? c[2] - r[2] : 0; z <= std::min(res[2] - 1, c[2] + r[2]); ++z)
+                for (uint32_t y = c[1] > r[1] ? c[1] - r[1] : 0; y <= std::min(res[1] - 1, c[1] + r[1]); ++y)
+                    for (uint32_t x = c[0] > r[0] ? c[0] - r[0] : 0; x <= std::min(res[0] - 1, c[0] + r[0]); ++x)
+                        if (plane || U(rng) < 0.3f) occ[((size_t)z * res[1] + y) * res[0] + x] = 1;
+        }
+        const uint32_t n0 = res[0] + 1, n1 = res[1] + 1, n2 = res[2] + 1;
+        std::vector<uint32_t> sat((size_t)n0 * n1 * n2, 0);
+        for (uint32_t z = 0; z < res[2]; ++z)
+            for (uint32_t y = 0; y < res[1]; ++y)
+                for (uint32_t x = 0; x < res[0]; ++x)
+                    sat[((size_t)(z + 1) * n1 + y + 1) * n0 + x + 1] = occ[((size_t)z * res[1] + y) * res[0] + x];
+        for (uint32_t z = 0; z < n2; ++z)          // prefix along x, then y, then z
+            for (uint32_t y = 0; y < n1; ++y)
+                for (uint32_t x = 1; x < n0; ++x) sat[((size_t)z * n1 + y) * n0 + x] += sat[((size_t)z * n1 + y) * n0 + x - 1];
+        for (uint32_t z = 0; z < n2; ++z)
+            for (uint32_t y = 1; y < n1; ++y)
+                for (uint32_t x = 0; x < n0; ++x) sat[((size_t)z * n1 + y) * n0 + x] += sat[((size_t)z * n1 + y - 1) * n0 + x];
+        for (uint32_t z = 1; z < n2; ++z)
+            for (uint32_t y = 0; y < n1; ++y)
+                for (uint32_t x = 0; x < n0; ++x) sat[((size_t)z * n1 + y) * n0 + x] += sat[((size_t)(z - 1) * n1 + y) * n0 + x];
+        EscSat S{sat.data(), n0, n0 * n1};
+        for (int q = 0; q < 200; ++q) {            // box queries against a direct count
+            uint32_t lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = rng() % res[a];
+                hi[a] = lo[a] + rng() % (res[a] - lo[a]);
+            }
+            uint32_t cnt = 0;
+            for (uint32_t z = lo[2]; z <= hi[2]; ++z)
+                for (uint32_t y = lo[1]; y <= hi[1]; ++y)
+                    for (uint32_t x = lo[0]; x <= hi[0]; ++x) cnt += occ[((size_t)z * res[1] + y) * res[0] + x];
+            if (esc_box(S, lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]) != cnt) ++box_fails;
+        }
+        const uint32_t nb[3] = {(res[0] + 3) / 4, (res[1] + 3) / 4, (res[2] + 3) / 4};
+        std::vector<uint8_t> tab((size_t)nb[0] * nb[1] * nb[2] * kEscNBin);
+        for (uint32_t bz = 0; bz < nb[2]; ++bz)
+            for (uint32_t by = 0; by < nb[1]; ++by)
+                for (uint32_t bx = 0; bx < nb[0]; ++bx)
+                    for (uint32_t bin = 0; bin < kEscNBin; ++bin) {
+                        const bool e = esc_compute(S, res, cs, bx, by, bz, bin);
+                        tab[(((size_t)bz * nb[1] + by) * nb[0] + bx) * kEscNBin + bin] = e;
+                        bits_set += e;
+                        ++bits;
+                    }
+        const GridK k{res[0] - 1, res[1] - 1, res[2] - 1, res[0], res[0] * res[1]};
+        for (int r = 0; r < n_rays; ++r) {
+            float c[3];
+            for (int a = 0; a < 3; ++a) {
+                const float ext = bmax[a] - bmin[a];
+                c[a] = r % 3 == 0 ? bmin[a] - 0.5f * ext + 2.0f * ext * U(rng) : bmin[a] + ext * U(rng);
+                if (r % 7 == 0) c[a] = bmin[a] + cs[a] * (float)(rng() % (res[a] + 1));   // on cell corners
+            }
+            v3 d;
+            if (r % 5 == 0) {                                                          // diagonals: face ties
+                d = normalize(mk((rng() & 1) ? 1.0f : -1.0f, (rng() & 1) ? 1.0f : -1.0f, (rng() & 1) ? 1.0f : -1.0f));
+            } else {
+                d = normalize(mk(U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f));
+            }
+            Dda s;
+            if (!dda_init(bmin, bmax, res, cs, mk(c[0], c[1], c[2]), d, s)) continue;
+            ++rays;
+            const bool usable = s.neg < 8u;
+            const uint32_t bin = esc_dir_bin(d);
+            bool escaped = false;
+            for (int guard = 0; guard < 100000; ++guard) {
+                ++steps;
+                const bool o = occ[((size_t)s.c2 * res[1] + s.c1) * res[0] + s.c0] != 0;
+                if (escaped) {
+                    ++saved;
+                    if (o) { ++unsound; break; }
+                }
+                const size_t brk = ((size_t)(s.c2 / 4) * nb[1] + s.c1 / 4) * nb[0] + s.c0 / 4;
+                if (!escaped && usable && tab[brk * kEscNBin + bin]) { escaped = true; ++escapes; }
+                bool crossed;
+                float te;
+                DDA_STEP(s, k, 2, crossed, te);
+                (void)crossed;
+                if (te == kInf) break;
+            }
+        }
+    }
+    printf("{\"rays\": %llu, \"steps\": %llu, \"escapes\": %llu, \"steps_after_escape\": %llu, \"bits_set\": %.4f, "
+           "\"unsound\": %llu, \"box_fails\": %llu}\n",
+           (unsigned long long)rays, (unsigned long long)steps, (unsigned long long)escapes,
+           (unsigned long long)saved, bits ? (double)bits_set / bits : 0.0, (unsigned long long)unsound,
+           (unsigned long long)box_fails);
+    return unsound || box_fails ? 1 : 0;
+}

@@ -243,7 +243,10 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 # The timed kernels (no counting build) against the oracle on every scene:
 # the default (wf_kernel primary launch, park + shade kernels for the
 # bounces) and per-lane walks everywhere (the fallback when OccX does not fit).
-MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK)]
+# The park walk with and without the escape table (escape.h) on every scene,
+# whatever the density rule picks by default.
+MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("escape", native.FLAG_ESCAPE),
+         ("no-escape", native.FLAG_NO_ESCAPE)]
 
 
 @pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])

@@ -8,7 +8,7 @@
 //            cells (begin, end) u32 x ncells, tri_pos 9 f32 x nrefs (v0, e1, e2)
 // rays.bin:  n u32, then (o, d) 6 f32 x n
 // out.bin:   per ray: steps u32, empty_steps u32, empty_entries u32,
-//            occ_steps u32, t f32, ref u32
+//            occ_steps u16 | last occupied-brick step << 16, t f32, ref u32
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
         const v3 o = mk(rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]);
         const v3 d = mk(rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]);
         float nearest = kInf;
-        uint32_t hidx = ~0u, steps = 0, esteps = 0, eent = 0, osteps = 0;
+        uint32_t hidx = ~0u, steps = 0, esteps = 0, eent = 0, osteps = 0, lastocc = 0;
         Dda s;
         if (dda_init(bmin, bmax, res, cs, o, d, s)) {
             uint32_t pb = ~0u;
@@ -63,6 +63,7 @@ int main(int argc, char** argv) {
                     if (b != pb) ++eent;
                 } else {
                     ++osteps;
+                    lastocc = steps;
                 }
                 pb = b;
                 for (uint32_t j = cells[2 * s.lin]; j < cells[2 * s.lin + 1]; ++j) {
@@ -79,7 +80,7 @@ int main(int argc, char** argv) {
             }
         }
         uint32_t* w = &out[6ull * r];
-        w[0] = steps; w[1] = esteps; w[2] = eent; w[3] = osteps;
+        w[0] = steps; w[1] = esteps; w[2] = eent; w[3] = osteps | (lastocc << 16);
         memcpy(&w[4], &nearest, 4);
         w[5] = hidx;
     }

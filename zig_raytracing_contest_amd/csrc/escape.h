@@ -1,0 +1,118 @@
+// Escape table for the park walk (render.hip wf_park_kernel), shared by the
+// device build kernel and the host check tests/cpp/escape_check.cpp.
+//
+// traceRay (stage3.zig:152-185) tests the triangles of every cell the DDA
+// visits until nearest <= t_next_crossing.  If no cell after the current one
+// holds a triangle, nothing after it can change the result: the walk may
+// stop there with the nearest hit so far (a miss stays +inf).  The table
+// proves that conservatively, per 4^3 brick B and direction bin:
+//   * a bin is a cone of directions: the dominant axis a and its sign (the
+//     cube face), and the slopes u = d_b / |d_a|, v = d_c / |d_a| of the
+//     other two axes in one of kEscBins x kEscBins cells of [-1, 1]^2;
+//   * the bit is set when the region swept by every ray that starts in B with
+//     a direction in the cone (its slopes widened by kEscEps), dilated by one
+//     cell on every side, holds no occupied cell of the grid.
+// A DDA walk is the ray's line up to f32 rounding, far below a cell, so every
+// cell it visits after one in B lies in that region: a set bit means every
+// later cell is empty.  Rays whose crossing sequences start at -inf / NaN (a
+// zero direction component on a cell boundary, Dda.neg bit 3) never use it.
+//
+// The region is tested slab by slab along a: the cells of slab i that the
+// cone can reach form a rectangle in the other two axes, and a summed-area
+// table of cell occupancy answers "any occupied cell in it" with 8 loads.
+#pragma once
+#include <stdint.h>
+
+#include "zrt_math.h"
+
+namespace zrt {
+
+constexpr uint32_t kEscBins = 4;                               // per face axis
+constexpr uint32_t kEscNBin = 6 * kEscBins * kEscBins;         // 96 bins
+constexpr uint32_t kEscWords = 4;                              // u32 words per brick (96 bits, padded)
+constexpr double kEscEps = 1e-3;                               // slope margin of a bin's cone
+
+// The bin of a direction (any consistent face choice on |d_a| ties: both
+// faces' cones hold the direction, their slopes reach +-1 + kEscEps).
+ZHD uint32_t esc_dir_bin(v3 d) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    uint32_t a;
+    float m, u, v;
+    // (the slopes need not be exact: a bin's cone is kEscEps wider than its
+    // cell, far more than the reciprocal's error)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ZRT_ESC_RCP(x) __builtin_amdgcn_rcpf(x)
+#else
+#define ZRT_ESC_RCP(x) (1.0f / (x))
+#endif
+    if (ax >= ay && ax >= az) { a = 0; m = d.x; const float r = ZRT_ESC_RCP(ax); u = d.y * r; v = d.z * r; }
+    else if (ay >= az) { a = 1; m = d.y; const float r = ZRT_ESC_RCP(ay); u = d.x * r; v = d.z * r; }
+    else { a = 2; m = d.z; const float r = ZRT_ESC_RCP(az); u = d.x * r; v = d.y * r; }
+#undef ZRT_ESC_RCP
+    const uint32_t f = 2u * a + (m < 0.0f ? 1u : 0u);
+    const float fb = (float)kEscBins;
+    const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * 0.5f * fb, 0.0f), fb - 1.0f);
+    const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 0.5f * fb, 0.0f), fb - 1.0f);
+    return (f * kEscBins + iu) * kEscBins + iv;
+}
+
+// Summed-area table of cell occupancy, (res0 + 1) x (res1 + 1) x (res2 + 1):
+// S[z][y][x] = occupied cells in [0, x) x [0, y) x [0, z).
+struct EscSat {
+    const uint32_t* s;
+    uint32_t n0, n01;      // res0 + 1, (res0 + 1) (res1 + 1)
+};
+// occupied cells in the inclusive cell box [x0, x1] x [y0, y1] x [z0, z1]
+ZHD uint32_t esc_box(const EscSat& S, uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1, uint32_t z0, uint32_t z1) {
+    const uint64_t X0 = x0, X1 = x1 + 1ull, Y0 = (uint64_t)y0 * S.n0, Y1 = (uint64_t)(y1 + 1) * S.n0;
+    const uint64_t Z0 = (uint64_t)z0 * S.n01, Z1 = (uint64_t)(z1 + 1) * S.n01;
+    return S.s[Z1 + Y1 + X1] - S.s[Z1 + Y1 + X0] - S.s[Z1 + Y0 + X1] + S.s[Z1 + Y0 + X0] - S.s[Z0 + Y1 + X1] +
+           S.s[Z0 + Y1 + X0] + S.s[Z0 + Y0 + X1] - S.s[Z0 + Y0 + X0];
+}
+
+// The bit of brick (bx, by, bz) and `bin` (see the header comment).
+ZHD bool esc_compute(const EscSat& S, const uint32_t res[3], const float cs[3], uint32_t bx, uint32_t by,
+                     uint32_t bz, uint32_t bin) {
+    const uint32_t fc = bin / (kEscBins * kEscBins), iu = (bin / kEscBins) % kEscBins, iv = bin % kEscBins;
+    const int a = (int)(fc / 2u), sg = (fc & 1u) ? -1 : 1;
+    const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+    const double nb = (double)kEscBins;
+    const double u0 = -1.0 + 2.0 * iu / nb - kEscEps, u1 = -1.0 + 2.0 * (iu + 1) / nb + kEscEps;
+    const double v0 = -1.0 + 2.0 * iv / nb - kEscEps, v1 = -1.0 + 2.0 * (iv + 1) / nb + kEscEps;
+    const uint32_t B[3] = {bx, by, bz};
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = 4.0 * B[k];
+        hi[k] = fmin(4.0 * B[k] + 4.0, (double)res[k]);
+    }
+    // a cell-unit step along a moves cs_a / cs_b cells along b
+    const double kb = (double)cs[a] / (double)cs[b], kc = (double)cs[a] / (double)cs[c];
+    const int ra = (int)res[a];
+    for (int i = sg > 0 ? (int)lo[a] : (int)hi[a] - 1; i >= 0 && i < ra; i += sg) {
+        double smin, smax;                      // a-distance from the brick to slab i
+        if (sg > 0) { smin = fmax(0.0, i - hi[a]); smax = fmax(0.0, i + 1.0 - lo[a]); }
+        else { smin = fmax(0.0, lo[a] - (i + 1.0)); smax = fmax(0.0, hi[a] - i); }
+        const double ylo = lo[b] + kb * fmin(smin * u0, smax * u0), yhi = hi[b] + kb * fmax(smin * u1, smax * u1);
+        const double zlo = lo[c] + kc * fmin(smin * v0, smax * v0), zhi = hi[c] + kc * fmax(smin * v1, smax * v1);
+        // the cells the interval touches, one more on each side
+        const double yf0 = floor(ylo) - 1.0, yf1 = ceil(yhi), zf0 = floor(zlo) - 1.0, zf1 = ceil(zhi);
+        if (yf1 < 0.0 || yf0 > res[b] - 1.0 || zf1 < 0.0 || zf0 > res[c] - 1.0) {
+            // the region lies beside the grid in this slab; it only moves
+            // further out when neither slope range straddles 0 on that side
+            const bool out_y = (yf1 < 0.0 && u1 <= 0.0) || (yf0 > res[b] - 1.0 && u0 >= 0.0);
+            const bool out_z = (zf1 < 0.0 && v1 <= 0.0) || (zf0 > res[c] - 1.0 && v0 >= 0.0);
+            if (out_y || out_z) break;
+            continue;
+        }
+        const uint32_t y0 = (uint32_t)fmax(0.0, yf0), y1 = (uint32_t)fmin(res[b] - 1.0, yf1);
+        const uint32_t z0 = (uint32_t)fmax(0.0, zf0), z1 = (uint32_t)fmin(res[c] - 1.0, zf1);
+        uint32_t lo3[3], hi3[3];
+        lo3[a] = hi3[a] = (uint32_t)i;
+        lo3[b] = y0; hi3[b] = y1;
+        lo3[c] = z0; hi3[c] = z1;
+        if (esc_box(S, lo3[0], hi3[0], lo3[1], hi3[1], lo3[2], hi3[2]) != 0u) return false;
+    }
+    return true;
+}
+
+}  // namespace zrt

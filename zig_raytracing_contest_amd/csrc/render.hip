@@ -30,6 +30,7 @@
 
 #include "zrt_internal.h"
 #include "dda.h"
+#include "escape.h"
 #include "device_geometry.h"
 
 using namespace zrt;
@@ -81,6 +82,18 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // cells lie in empty bricks, ~4 cells per brick entered, tools/walk_sim.cpp)
 #ifndef ZRT_PRIM_SKIP
 #define ZRT_PRIM_SKIP 0
+#endif
+// ZRT_ESCAPE: the park walk stops a segment once its escape-table bit
+// (escape.h) says every later cell of its ray is empty
+#ifndef ZRT_ESCAPE
+#define ZRT_ESCAPE 1
+#endif
+// (measurement variants: queries without the check / the check without queries)
+#ifndef ZRT_ESC_NOCHECK
+#define ZRT_ESC_NOCHECK 0
+#endif
+#ifndef ZRT_ESC_NODMA
+#define ZRT_ESC_NODMA 0
 #endif
 // ZRT_PARK_MISS: a bounce segment that misses ends in the park kernel
 // (terminal radiance = the sky colour, stage3.zig:195-197), so the shade
@@ -548,6 +561,9 @@ struct WfParams {
     uint32_t occx_ldsw;       // u32 words OccX takes in LDS (multiple of 4): entries + masks
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
+    // escape table (escape.h): kEscWords u32 per 4^3 brick, bit b of word
+    // w = direction bin 32 w + b; null: not built (the walk never stops early)
+    const uint32_t* esc;
 };
 
 // Work / append counters: one per 128-byte line (32 u32), so the waves'
@@ -926,6 +942,20 @@ __device__ __forceinline__ void park_load_cell(const TraceParams& p, uint32_t pc
                  : "memory");
 }
 
+// The escape-table word of a walking lane's current brick into its wave's
+// escape slot esc[lane] (same LDS-DMA as park_load_range: no VGPR is written,
+// the walk never waits for it; the lane reads the slot at the next trips,
+// and a word for an earlier brick of the same ray is as valid as the current
+// one: every cell after it lies on the ray further on).
+__device__ __forceinline__ void park_load_esc(const uint32_t* word, uint32_t* esc) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)esc);
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "global_load_lds_dword %0, off"
+                 :
+                 : "v"(word), "s"(m0)
+                 : "memory");
+}
+
 // Per-wave LDS of the test rounds.
 struct ParkSlot {
     float4 o[64];                    // lane's ray origin; w: nearest entering the round
@@ -961,7 +991,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -971,11 +1001,15 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 #define PARK_COUNT(k, v) do { } while (0)
 #endif
 
+// ESC: with the escape table (context_escape decides per scene)
+template <bool ESC>
 __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
     uint32_t* const rng_slot = s_rng + 192u * (threadIdx.x >> 6);
+    __shared__ uint32_t s_esc[kParkWaves * 64];             // escape-table words (park_load_esc)
+    uint32_t* const esc_slot = s_esc + 64u * (threadIdx.x >> 6);
     __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
     for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
         SEL8_ENTRY(i, pos);
@@ -1015,6 +1049,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
     uint32_t pitem = 0, pmask = 0;         // ZRT_PARK_MISS: its item and scatter mask
+    // the ray's escape-table word (byte offset in a brick's kEscWords) and
+    // bit; emask 0: the ray never stops early (no table, or a -inf / NaN
+    // crossing sequence)
+    uint32_t eoff = 0, emask = 0;
+    uint32_t eb = ~0u;                     // the brick of the lane's last escape-table query
     PARK_PROF_DECL
 
     for (;;) {
@@ -1078,6 +1117,15 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                             Dda s0;
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
                                 ddav_from(s0, gk, pk, s);
+                                if (ESC) {
+                                    // (every DMA into this slot from the lane's last
+                                    // ray has landed: its kDone drained vmcnt above)
+                                    const uint32_t bin = esc_dir_bin(d);
+                                    eoff = (bin >> 5) * 4u;
+                                    emask = w.esc && s0.neg < 8u ? 1u << (bin & 31u) : 0u;
+                                    eb = ~0u;
+                                    esc_slot[lane] = 0u;
+                                }
                                 if (occx_cell(occx_mask(L, occx_brick(w, s)), s, pk)) {
                                     park_load_range(p, s.pc, rng_slot);
                                     rng_slot[128 + lane] = ~0u;    // first cell: every ref
@@ -1118,6 +1166,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 // four execz branches with per-lane booleans, r03p)
                 constexpr int kS = ZRT_WALK_STEPS;
                 static_assert(kS >= 2, "the trip keeps the cell before its last step");
+                // the escape words landed so far (used at the trip's end, so the
+                // read's latency hides behind the trip)
+                const uint32_t ew = ESC ? esc_slot[lane] & emask : 0u;
                 DdaV ss[kS];
                 LaneM ex[kS], stop[kS], dd[kS];
                 float te[kS];
@@ -1176,6 +1227,23 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                                                       : ((x & pk.f1) ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
                     park_load_cell(p, s.pc, face, rng_slot);
                     st = kPark;
+                }
+                if (ESC) {
+                    // a set escape bit: no cell of the ray after the queried
+                    // brick holds a triangle, so the hit so far stands (this
+                    // trip cannot have parked the lane: escape.h)
+                    const LaneM esc = lm_and(lm_of(st == kWalk), lm_of(ew != 0u));
+                    PARK_COUNT(16, __popcll(esc));
+                    if (!ZRT_ESC_NOCHECK) st = lm_selu(esc, kDone, st);
+                    // one query per brick the ray enters (its word does not
+                    // change while the lane walks inside the brick)
+                    const uint32_t b = occx_brick(w, s);
+                    if (!ZRT_ESC_NODMA && st == kWalk && emask != 0u && b != eb) {
+                        park_load_esc(reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(w.esc) +
+                                                                        b * (4u * kEscWords) + eoff),
+                                      esc_slot);
+                        eb = b;
+                    }
                 }
             }
         }
@@ -1249,7 +1317,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
     if (lane == 0)
-        for (int k = 13; k < 16; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
+        for (int k = 13; k < 17; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
 #endif
 }
 
@@ -1620,7 +1688,8 @@ constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that ru
 constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256 -
-                                256 * 8;   // the select table
+                                256 * 8 -   // the select table
+                                kParkWaves * 64 * 4;   // the escape slots
 
 }  // namespace
 
@@ -1644,6 +1713,9 @@ struct zrt_context {
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
+    uint32_t* d_esc = nullptr;      // escape table (escape.h), with OccX
+    bool esc_on = false;            // the park launches use it (dense enough to pay, context_escape)
+    double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
     // grow-only work buffers
@@ -1735,7 +1807,7 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelE,wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelILb1E,wf_park_kernelILb0E,wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(
         ZRT_WF_MINW) "ELb0ELb1EE";
 #undef ZRT_STR
 #undef ZRT_STR2
@@ -1760,7 +1832,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->d_cell32) (void)hipFree(c->d_cell32);
-    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx,
+    void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_esc,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2061,6 +2133,98 @@ __global__ __launch_bounds__(kBlock) void occ_cells_kernel(const uint2* __restri
     }
 }
 
+// Escape table (escape.h): a summed-area table of cell occupancy, then one
+// thread per (4^3 brick, direction bin).
+__global__ __launch_bounds__(kBlock) void esc_sat_fill_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
+                                                              uint32_t ncells, uint32_t n0, uint32_t n01,
+                                                              uint32_t* __restrict__ sat) {
+    for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
+        const uint2 c = cells[ci];
+        const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / r0 / r1;
+        sat[(uint64_t)(z + 1) * n01 + (uint64_t)(y + 1) * n0 + x + 1] = c.x < c.y ? 1u : 0u;
+    }
+}
+// prefix sums along one axis of the (n0 x n1 x n2) volume: one thread per line
+__global__ __launch_bounds__(kBlock) void esc_sat_scan_kernel(uint32_t* __restrict__ sat, uint32_t n0, uint32_t n1,
+                                                              uint32_t n2, uint32_t axis) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t n01 = (uint64_t)n0 * n1;
+    uint64_t base, stride;
+    uint32_t len;
+    if (axis == 0) {
+        if (t >= n1 * n2) return;
+        base = (uint64_t)(t / n1) * n01 + (uint64_t)(t % n1) * n0; stride = 1; len = n0;
+    } else if (axis == 1) {
+        if (t >= n0 * n2) return;
+        base = (uint64_t)(t / n0) * n01 + t % n0; stride = n0; len = n1;
+    } else {
+        if (t >= n0 * n1) return;
+        base = t; stride = n01; len = n2;
+    }
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < len; ++i) {
+        acc += sat[base + i * stride];
+        sat[base + i * stride] = acc;
+    }
+}
+__global__ __launch_bounds__(kBlock) void esc_build_kernel(const uint32_t* __restrict__ sat, uint32_t r0, uint32_t r1,
+                                                           uint32_t r2, float cs0, float cs1, float cs2, uint32_t nb0,
+                                                           uint32_t nb1, uint32_t nbr, uint32_t* __restrict__ esc) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (uint64_t)nbr * kEscNBin) return;
+    const uint32_t br = (uint32_t)(t / kEscNBin), bin = (uint32_t)(t % kEscNBin);
+    const uint32_t res[3] = {r0, r1, r2};
+    const float cs[3] = {cs0, cs1, cs2};
+    const EscSat S{sat, r0 + 1u, (r0 + 1u) * (r1 + 1u)};
+    if (esc_compute(S, res, cs, br % nb0, (br / nb0) % nb1, br / (nb0 * nb1), bin))
+        atomicOr(&esc[(uint64_t)br * kEscWords + (bin >> 5)], 1u << (bin & 31u));
+}
+
+// Least fraction of set escape bits for the park launches to use the table.
+constexpr double kEscMinDensity = 0.12;
+// The escape table for a context with OccX (the park walk); none for grids
+// whose summed-area table would pass 2^28 entries (the walk then never stops
+// early, as before).
+static int context_escape(zrt_context* c) {
+    if (!ZRT_ESCAPE || !c->occx_ok) return ZRT_OK;
+    const uint32_t* r = c->grid.resolution;
+    const uint64_t n0 = r[0] + 1ull, n1 = r[1] + 1ull, n2 = r[2] + 1ull;
+    if (n0 * n1 * n2 > (1ull << 28)) return ZRT_OK;
+    const uint64_t nbr = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
+    struct Scratch {
+        uint32_t* sat = nullptr;
+        ~Scratch() { if (sat) (void)hipFree(sat); }
+    } tmp;
+    HIP_TRY(hipMalloc((void**)&tmp.sat, 4ull * n0 * n1 * n2));
+    HIP_TRY(hipMalloc((void**)&c->d_esc, 4ull * kEscWords * nbr));
+    HIP_TRY(hipMemsetAsync(tmp.sat, 0, 4ull * n0 * n1 * n2, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_esc, 0, 4ull * kEscWords * nbr, c->stream));
+    hipLaunchKernelGGL(esc_sat_fill_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells,
+                       (uint32_t)n0, (uint32_t)(n0 * n1), tmp.sat);
+    const uint64_t lines[3] = {n1 * n2, n0 * n2, n0 * n1};
+    for (uint32_t a = 0; a < 3; ++a)
+        hipLaunchKernelGGL(esc_sat_scan_kernel, dim3((uint32_t)((lines[a] + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           c->stream, tmp.sat, (uint32_t)n0, (uint32_t)n1, (uint32_t)n2, a);
+    const uint64_t nthr = nbr * kEscNBin;
+    hipLaunchKernelGGL(esc_build_kernel, dim3((uint32_t)((nthr + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       (const uint32_t*)tmp.sat, r[0], r[1], r[2], c->grid.cell_size[0], c->grid.cell_size[1],
+                       c->grid.cell_size[2], c->occx_nb[0], c->occx_nb[1], (uint32_t)nbr, c->d_esc);
+    HIP_TRY(hipGetLastError());
+    // Use it when enough of its bits are set: each walk trip of the park
+    // kernel then issues a table query per brick entered (~4% of a launch on
+    // scenes whose rays never escape, r04g), and the check itself costs ~1.5%.
+    // Measured (r04): contest stand-in 23% of the bits set, +8% frame rate;
+    // Cornell box 6%, -1.5%; Sponza-scale 1.6%, -4%.
+    std::vector<uint32_t> h(kEscWords * nbr);
+    HIP_TRY(hipMemcpyAsync(h.data(), c->d_esc, 4ull * kEscWords * nbr, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint64_t set = 0;
+    for (uint32_t x : h) set += (uint64_t)__builtin_popcount(x);
+    c->esc_density = (double)set / ((double)nbr * kEscNBin);
+    c->esc_on = c->esc_density >= kEscMinDensity;
+    return ZRT_OK;
+}
+
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     const uint32_t* r = c->grid.resolution;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
@@ -2178,6 +2342,8 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         c->occx_nbw = (uint32_t)nbw;
         c->occx_moff = (uint32_t)moff;
     }
+    int rc = context_escape(c);
+    if (rc != ZRT_OK) return rc;
     return context_counters(c);
 }
 
@@ -2488,7 +2654,12 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 #endif
     const bool packed = c->packed;
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
-    const WfFn f_next = park_next ? (WfFn)wf_park_kernel : (packed ? kWfBounce : kWfBounceWide);
+    // the escape table: where dense enough to pay (context_escape), or as
+    // the flags force it (both kernels give the same image)
+    const bool esc = c->d_esc && !(cfg->flags & ZRT_FLAG_NO_ESCAPE) &&
+                     (c->esc_on || (cfg->flags & ZRT_FLAG_ESCAPE));
+    const WfFn f_next = park_next ? (esc ? (WfFn)wf_park_kernel<true> : (WfFn)wf_park_kernel<false>)
+                                  : (packed ? kWfBounce : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
     const size_t lds_shade = c->nmat <= kLdsMats ? c->nmat * sizeof(DevMat) : 0;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
@@ -2670,6 +2841,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.occx_nb01 = c->occx_nb[0] * c->occx_nb[1];
             W.test_min = test_min;
             W.refill_min = refill_min;
+            W.esc = c->d_esc;
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? q0 : q1;
                 W.q_out = (k & 1) ? q1 : q0;
@@ -2754,7 +2926,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_walk_steps\": {\"lane_steps\": %llu, \"empty_brick_steps\": %llu, "
-                "\"empty_brick_entries\": %llu}}\n", hs[48], hs[49], hs[50]);
+                "\"empty_brick_entries\": %llu, \"escapes\": %llu}}\n", hs[48], hs[49], hs[50], hs[51]);
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);
