@@ -267,7 +267,10 @@ def roofline_profile_for(config, one_set_kernel="wf_park_kernel"):
     files = glob.glob(os.path.join(ROOT, "profiles", "r*", f"*_roofline_{config}.json"))
     if not files:
         return None
-    f = max(files, key=lambda x: (len(os.path.basename(x).split("_")[0]), os.path.basename(x)))
+    def order(x):                      # round, then tag: r03zm < r04a < r04ab
+        tag = os.path.basename(x).split("_")[0]
+        return (int(tag[1:3]) if tag[1:3].isdigit() else 0, len(tag), tag)
+    f = max(files, key=order)
     try:
         with open(f) as fh:
             d = json.load(fh)
