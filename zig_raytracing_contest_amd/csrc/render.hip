@@ -360,7 +360,8 @@ __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, floa
     const float* b = texels + t.off;
     if (ZRT_TEX1 && t.w == 1 && t.h == 1) {
         const float fu = tex_frac(u), fv = tex_frac(v);
-        const float x = b[0], y = b[1], z = b[2];
+        // the texel, inlined in the descriptor (dev_tex_inline)
+        const float x = __int_as_float(t.umin), y = __int_as_float(t.umax), z = __int_as_float(t.vmin);
         return mk(bilerp(x, x, x, x, fu, fv), bilerp(y, y, y, y, fu, fv), bilerp(z, z, z, z, fu, fv));
     }
     const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
@@ -373,7 +374,7 @@ __device__ __forceinline__ v3 sample3(const float* texels, const DevTex& t, floa
 __device__ __forceinline__ float sample1(const float* texels, const DevTex& t, float u, float v) {
     const float* b = texels + t.off;
     if (ZRT_TEX1 && t.w == 1 && t.h == 1) {               // the 1x1 dummy (see sample3)
-        const float x = b[0];
+        const float x = __int_as_float(t.umin);
         return bilerp(x, x, x, x, tex_frac(u), tex_frac(v));
     }
     const TexCoords c = tex_coords(t.w, t.h, t.umin, t.umax, t.vmin, t.vmax, u, v);
@@ -991,7 +992,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -1262,6 +1263,8 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             PARK_COUNT(5, 1);
             PARK_COUNT(6, (tot + 63u) / 64u);
             PARK_COUNT(7, tot);
+            PARK_COUNT(17, __popcll(__ballot(ready)));               // parked lanes tested
+            PARK_COUNT(18, __popcll(__ballot(ready && n == 0u)));    // ... with no ref left to test
             W.o[lane].w = nearest;
             rng_slot[lane] = rb;                                   // (the slots are free until the walk)
             rng_slot[64 + lane] = off;
@@ -1317,7 +1320,7 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
     if (lane == 0)
-        for (int k = 13; k < 17; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
+        for (int k = 13; k < 19; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
 #endif
 }
 
@@ -2073,6 +2076,7 @@ static int context_materials(zrt_context* c, const zrt_scene* s) {
             d.umin = t[k]->u_min; d.umax = t[k]->u_max;
             d.vmin = t[k]->v_min; d.vmax = t[k]->v_max;
             d.pad = 0;
+            dev_tex_inline(d, s->texels, k < 2 ? 3 : 1);
         }
     }
     HIP_TRY(hipMalloc((void**)&c->d_mats, mats.size() * sizeof(DevMat)));
@@ -2926,7 +2930,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_walk_steps\": {\"lane_steps\": %llu, \"empty_brick_steps\": %llu, "
-                "\"empty_brick_entries\": %llu, \"escapes\": %llu}}\n", hs[48], hs[49], hs[50], hs[51]);
+                "\"empty_brick_entries\": %llu, \"escapes\": %llu, \"parked_tested\": %llu, \"parked_no_refs\": %llu}}\n",
+                hs[48], hs[49], hs[50], hs[51], hs[52], hs[53]);
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);
@@ -3128,6 +3133,7 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             DevTex t;
             t.off = 0; t.w = h[1]; t.h = h[2]; t.umin = h[3]; t.umax = h[4]; t.vmin = h[5]; t.vmax = h[6];
             const float* tex = (const float*)(h + 8);
+            dev_tex_inline(t, tex, h[0]);
             const float* a = (const float*)in + 2ull * i;
             float* o = (float*)out + 3ull * i;
             if (h[0] == 3) {

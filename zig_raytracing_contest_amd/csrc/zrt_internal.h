@@ -1,5 +1,6 @@
 // zrt_internal.h -- types shared by the host code and the CDNA4 kernels.
 #pragma once
+#include <cstring>
 
 #include "../../include/zrt.h"
 #include "zrt_math.h"
@@ -14,6 +15,16 @@ struct DevTex {
     uint32_t pad;
 };
 struct DevMat { DevTex tex[3]; };   // base_color, emissive, transparency
+// A 1x1 texture (every material slot without an image, stage1.zig:411-425)
+// needs no clamp range (any clamp and @mod by 1 give texel 0), so its texel
+// rides in those fields instead: channel k's f32 bits in (umin, umax,
+// vmin)[k].  Sampling then reads it from the material (LDS in the shade
+// kernel) instead of the texel pool.
+ZHD void dev_tex_inline(DevTex& d, const float* texels, int chans) {
+    if (d.w != 1 || d.h != 1) return;
+    int32_t* f[3] = {&d.umin, &d.umax, &d.vmin};
+    for (int k = 0; k < chans; ++k) memcpy(f[k], texels + d.off + k, 4);
+}
 
 // Ziggurat NormDist tables (Zig std ziggurat.zig ZigTableGen), computed on the
 // host with the deterministic exp/log of zrt_math.h.
