@@ -360,7 +360,8 @@ def main():
     soup = scenes.get_scene(cfgd["scene"])
     cam = camera_for(soup, cfgd["camera"], cfgd["width"], cfgd["height"])
     rs = RenderScene(soup, device=local)
-    P = native.tile_pixels(cam.w, cam.h, 64, rank, world).size
+    TILE = zdist.TILE                # the multi-rank tile edge (any tiling gives the same image)
+    P = native.tile_pixels(cam.w, cam.h, TILE, rank, world).size
     dev_buf = None
     if world > 1 and not gloo:
         dev_buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8,
@@ -375,7 +376,7 @@ def main():
                                              dev_buf, stats=stats)
             return res["stats"], img
         res = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world, stats=stats,
-                                packed=True, flags=flags)
+                                packed=True, flags=flags, tile=TILE)
         if world > 1:                # gloo: host copies
             buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8)
             buf[: res["packed"].size] = torch.from_numpy(res["packed"].reshape(-1))
@@ -388,7 +389,7 @@ def main():
             return None
         if world == 1:
             full = np.zeros((cam.w * cam.h, 3), np.uint8)
-            full[native.tile_pixels(cam.w, cam.h)] = img
+            full[native.tile_pixels(cam.w, cam.h, TILE)] = img
             return hashlib.sha1(full.tobytes()).hexdigest()
         return hashlib.sha1(img.cpu().numpy().tobytes()).hexdigest()
 
@@ -438,7 +439,7 @@ def main():
         # every launch: exclusive per-kernel durations (what the committed
         # rocprofv3 profile of `bench.py --one-set` reports).
         rres = rs.context.render(cam, spp, cfgd["max_bounce"], rank=rank, num_ranks=world, packed=True,
-                                 flags=native.FLAG_ONE_SET | native.FLAG_KERNEL_TIMES)
+                                 flags=native.FLAG_ONE_SET | native.FLAG_KERNEL_TIMES, tile=TILE)
         rprof = rs.context.profile()
         if world == 1:
             assert frame_sha1(rres["packed"]) == img_sha1, "the one-stream frame differs"

@@ -156,7 +156,7 @@ dist.init_process_group("gloo", rank=rank, world_size=world)
 soup = scenes.get_scene("contest")
 cam = camera_for(soup, "Camera 1", None, 180)
 rs = RenderScene(soup, device=0)
-res = rs.context.render(cam, 2, 4, rank=rank, num_ranks=world, packed=True)
+res = rs.context.render(cam, 2, 4, rank=rank, num_ranks=world, packed=True, tile=zdist.TILE)
 buf = torch.zeros(zdist.max_packed(cam.w, cam.h, world) * 3, dtype=torch.uint8)
 buf[: res["packed"].size] = torch.from_numpy(res["packed"].reshape(-1))
 img = zdist.gather_image(buf, cam.w, cam.h, rank, world, dist)

@@ -51,7 +51,9 @@ def test_gather_tiles_gloo(world, w, h):
     pix = np.arange(w * h)
     assert np.array_equal(img[..., 0].reshape(-1), (pix % 251).astype(np.uint8))
     assert np.array_equal(img[..., 1].reshape(-1), ((pix // 251) % 253).astype(np.uint8))
-    # tile t belongs to rank t % world
-    tx = (w + 63) // 64
-    owner = (((pix // w) // 64) * tx + (pix % w) // 64) % world
+    # tile t (zdist.TILE pixels square) belongs to rank t % world
+    from zig_raytracing_contest_amd import dist as zdist
+    T = zdist.TILE
+    tx = (w + T - 1) // T
+    owner = (((pix // w) // T) * tx + (pix % w) // T) % world
     assert np.array_equal(img[..., 2].reshape(-1), owner.astype(np.uint8))

@@ -27,9 +27,12 @@
 
 namespace zrt {
 
-constexpr uint32_t kEscBins = 4;                               // per face axis
-constexpr uint32_t kEscNBin = 6 * kEscBins * kEscBins;         // 96 bins
-constexpr uint32_t kEscWords = 4;                              // u32 words per brick (96 bits, padded)
+#ifndef ZRT_ESC_BINS
+#define ZRT_ESC_BINS 8
+#endif
+constexpr uint32_t kEscBins = ZRT_ESC_BINS;                    // per face axis
+constexpr uint32_t kEscNBin = 6 * kEscBins * kEscBins;         // 384 bins (r04q: 8 x 8 per face vs 4 x 4: cfg3 +0.9%)
+constexpr uint32_t kEscWords = kEscNBin <= 128 ? 4 : (kEscNBin + 31) / 32;   // u32 words per brick
 constexpr double kEscEps = 1e-3;                               // slope margin of a bin's cone
 
 // The bin of a direction (any consistent face choice on |d_a| ties: both

@@ -14,12 +14,19 @@ import numpy as np
 
 from . import native
 
+# Tile edge of the multi-rank split: 32x32 tiles balance 8 ranks to a max/mean
+# per-rank time of 1.008 on cfg3 (64x64: 1.039), strong-scaling efficiency
+# 0.934 vs 0.906 predicted from every rank's tile set on one GPU
+# (tools/rank_time.py, profiles/r04/r04q_rank_time_tiles.log); the image is
+# the same for any tile size.
+TILE = 32
 
-def rank_pixels(w: int, h: int, rank: int, world: int, tile: int = 64) -> np.ndarray:
+
+def rank_pixels(w: int, h: int, rank: int, world: int, tile: int = TILE) -> np.ndarray:
     return native.tile_pixels(w, h, tile, rank, world)
 
 
-def max_packed(w: int, h: int, world: int, tile: int = 64) -> int:
+def max_packed(w: int, h: int, world: int, tile: int = TILE) -> int:
     return max(rank_pixels(w, h, r, world, tile).size for r in range(world))
 
 
@@ -35,7 +42,7 @@ def _indices(w, h, world, tile, device):
     return _IDX[key]
 
 
-def gather_image(packed, w: int, h: int, rank: int, world: int, dist, tile: int = 64):
+def gather_image(packed, w: int, h: int, rank: int, world: int, dist, tile: int = TILE):
     """packed: 1-D uint8 torch tensor of max_packed(...)*3 bytes on this rank's
     device (only the first n_rank*3 bytes are meaningful).  Returns the
     assembled (h, w, 3) uint8 tensor on rank 0 (same device), None elsewhere;
@@ -52,7 +59,7 @@ def gather_image(packed, w: int, h: int, rank: int, world: int, dist, tile: int 
 
 
 def render_gathered(context, cam, spp: int, max_bounce: int, rank: int, world: int, dist, dev_buf,
-                    stats: bool = False, tile: int = 64):
+                    stats: bool = False, tile: int = TILE):
     """One frame of bench.py's multi-GPU step: this rank's tiles rendered
     straight into `dev_buf` (a device tensor of max_packed(...)*3 bytes,
     zrt_outputs.device_rgb_packed: no host copy), then gather_image to rank 0.
