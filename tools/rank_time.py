@@ -18,7 +18,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg3")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--ranks", default="1,2,4,8")
-ap.add_argument("--tile", type=int, default=64, help="square tile edge (zrt_render_config.tile_size)")
+ap.add_argument("--tile", type=int, default=32, help="square tile edge (zrt_render_config.tile_size; bench.py: dist.TILE)")
+ap.add_argument("--spp-pass", type=int, default=0, help="zrt_render_config.samples_per_pass (0 = automatic)")
 a = ap.parse_args()
 cfg = scenes.CONFIGS[a.config]
 soup = scenes.get_scene(cfg["scene"])
@@ -29,11 +30,13 @@ t1 = seg1 = None
 for n in [int(x) for x in a.ranks.split(",")]:
     per = {}
     for r in range(n):
-        ctx.render(cam, cfg["spp"], cfg["max_bounce"], rank=r, num_ranks=n, tile=a.tile)     # warm
+        ctx.render(cam, cfg["spp"], cfg["max_bounce"], rank=r, num_ranks=n, tile=a.tile,
+                   samples_per_pass=a.spp_pass)     # warm
         ts = []
         for _ in range(a.reps):
             t0 = time.perf_counter()
-            st = ctx.render(cam, cfg["spp"], cfg["max_bounce"], rank=r, num_ranks=n, tile=a.tile)["stats"]
+            st = ctx.render(cam, cfg["spp"], cfg["max_bounce"], rank=r, num_ranks=n, tile=a.tile,
+                            samples_per_pass=a.spp_pass)["stats"]
             ts.append(time.perf_counter() - t0)
         prof = ctx.profile()
         per[r] = (min(ts), st["segments"], st["trace_kernel_ms"], prof["passes"], prof["sets"])
@@ -42,7 +45,7 @@ for n in [int(x) for x in a.ranks.split(",")]:
     segs = sum(v[1] for v in per.values())
     if n == 1:
         t1, seg1 = tmax, segs
-    print(json.dumps({"config": a.config, "ranks": n, "tile": a.tile,
+    print(json.dumps({"config": a.config, "ranks": n, "tile": a.tile, "spp_pass": a.spp_pass,
                       "ms_per_rank": {r: round(v[0] * 1e3, 2) for r, v in per.items()},
                       "segments": {r: v[1] for r, v in per.items()},
                       "passes_sets": {r: [v[3], v[4]] for r, v in per.items()},

@@ -7,7 +7,7 @@
 // scene.bin: bbox[6] f32, res[3] u32, cs[3] f32, ncells u32, nrefs u32,
 //            cells (begin, end) u32 x ncells, tri_pos 9 f32 x nrefs (v0, e1, e2)
 // rays.bin:  n u32, then (o, d) 6 f32 x n
-// out.bin:   per ray: steps u32, empty_steps u32, empty_entries u32,
+// out.bin:   per ray: steps u16 | first occupied-cell step << 16, empty_steps u32, empty_entries u32,
 //            occ_steps u16 | last occupied-brick step << 16, t f32, ref u32
 #include <cstdio>
 #include <cstdlib>
@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
         const v3 o = mk(rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]);
         const v3 d = mk(rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]);
         float nearest = kInf;
-        uint32_t hidx = ~0u, steps = 0, esteps = 0, eent = 0, osteps = 0, lastocc = 0;
+        uint32_t hidx = ~0u, steps = 0, esteps = 0, eent = 0, osteps = 0, lastocc = 0, firstocc = 0;
         Dda s;
         if (dda_init(bmin, bmax, res, cs, o, d, s)) {
             uint32_t pb = ~0u;
@@ -66,6 +66,7 @@ int main(int argc, char** argv) {
                     lastocc = steps;
                 }
                 pb = b;
+                if (!firstocc && cells[2 * s.lin + 1] > cells[2 * s.lin]) firstocc = steps;
                 for (uint32_t j = cells[2 * s.lin]; j < cells[2 * s.lin + 1]; ++j) {
                     const float* q = &tp[9ull * j];
                     float t, u, v;
@@ -80,7 +81,7 @@ int main(int argc, char** argv) {
             }
         }
         uint32_t* w = &out[6ull * r];
-        w[0] = steps; w[1] = esteps; w[2] = eent; w[3] = osteps | (lastocc << 16);
+        w[0] = steps | (firstocc << 16); w[1] = esteps; w[2] = eent; w[3] = osteps | (lastocc << 16);
         memcpy(&w[4], &nearest, 4);
         w[5] = hidx;
     }
