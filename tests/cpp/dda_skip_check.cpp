@@ -206,6 +206,67 @@ static void walk_skipv(const TestGrid& g, const GridK& k, const Dda& s0, const s
     if (n != ref.size() && !(ref.size() == n + 1 && ref[n].c0 == ~0u)) ++g_skipv_fails;
 }
 
+// DDAV_FF (the primary walk's fast-forward) against the cell walk: from
+// random points of the walk, the packed state after every crossing with
+// t < tau must be the cell walk's state after its steps with TC < tau (ts bit
+// for bit, same cell), and EXITED must be set exactly when the cell walk meets
+// its exit crossing among them.
+static uint64_t g_ff_fails = 0, g_ff = 0, g_ff_steps = 0;
+static void walk_ff(const GridK& k, const Dda& s0, std::mt19937_64& rng) {
+    const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
+    PackK pk;
+    if (!pack_layout(res, pk) || s0.neg >= 8u) return;
+    Dda q = s0;
+    for (int guard = 0; guard < 100000; ++guard) {
+        if (rng() % 3 == 0) {                       // fast-forward from here
+            DdaV x;
+            ddav_from(q, k, pk, x);
+            const float tmin = fminf(q.tn0, fminf(q.tn1, q.tn2));
+            const float dmin = fminf(q.td0, fminf(q.td1, q.td2));
+            const float tau = tmin + (float)(1 + rng() % 120) * dmin;
+            bool exited, exited4, exitedc;
+            DdaV x4 = x, xc = x;
+            DDAV_FF(x, pk.f0, pk.f1, pk.f2, tau, exited);
+            DDAV_FF4(x4, pk.f0, pk.f1, pk.f2, tau, exited4);
+            DDAV_FFC(xc, pk, pk.f0, pk.f1, pk.f2, tau, exitedc);
+            if (exited4 != exited || (!exited && (x4.pc != x.pc || memcmp(&x4.tn0, &x.tn0, 4) ||
+                                                  memcmp(&x4.tn1, &x.tn1, 4) || memcmp(&x4.tn2, &x.tn2, 4)))) {
+                ++g_ff_fails;
+                return;
+            }
+            if (exitedc != exited || (!exited && (xc.pc != x.pc || memcmp(&xc.tn0, &x.tn0, 4) ||
+                                                  memcmp(&xc.tn1, &x.tn1, 4) || memcmp(&xc.tn2, &x.tn2, 4)))) {
+                ++g_ff_fails;
+                return;
+            }
+            Dda r = q;                              // the cell walk: steps with TC < tau
+            bool rexit = false;
+            for (int g2 = 0; g2 < 100000; ++g2) {
+                Dda t = r;
+                bool cr;
+                float te;
+                DDA_STEP(t, k, 2, cr, te);
+                const float tc = fminf(r.tn0, fminf(r.tn1, r.tn2));   // the step's crossing t
+                if (!(tc < tau)) break;
+                if (te == kInf) { rexit = true; break; }
+                r = t;
+                ++g_ff_steps;
+            }
+            ++g_ff;
+            if (exited != rexit ||
+                (!exited && (x.pc != pack_cellv(pk, r.c0, r.c1, r.c2) || memcmp(&x.tn0, &r.tn0, 4) ||
+                             memcmp(&x.tn1, &r.tn1, 4) || memcmp(&x.tn2, &r.tn2, 4)))) {
+                ++g_ff_fails;
+                return;
+            }
+        }
+        bool cr;
+        float te;
+        DDA_STEP(q, k, 2, cr, te);
+        if (te == kInf) return;
+    }
+}
+
 int main(int argc, char** argv) {
     const int n_grids = argc > 1 ? atoi(argv[1]) : 40;
     const int n_rays = argc > 2 ? atoi(argv[2]) : 4000;
@@ -257,6 +318,7 @@ int main(int argc, char** argv) {
             const auto a = walk_cells(g, k, s);
             const auto b = walk_skip(g, k, s, &skips);
             walk_skipv(g, k, s, a);
+            walk_ff(k, s, rng);
             if (!(a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin()))) {
                 if (++fails <= 5)
                     fprintf(stderr, "MISMATCH grid %d ray %d: %zu vs %zu cells (o=%g,%g,%g d=%g,%g,%g)\n", gi, r,
@@ -264,11 +326,12 @@ int main(int argc, char** argv) {
             }
         }
     }
-    fails += g_texit_fails + g_walk_fails + g_skipv_fails;
+    fails += g_texit_fails + g_walk_fails + g_skipv_fails + g_ff_fails;
     printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, "
-           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"skipv\": %llu, \"skipv_fails\": %llu, \"fails\": %llu}\n",
+           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"skipv\": %llu, \"skipv_fails\": %llu, \"ff\": %llu, \"ff_steps\": %llu, \"ff_fails\": %llu, \"fails\": %llu}\n",
            (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
            (unsigned long long)g_texit_fails, (unsigned long long)g_walk_steps, (unsigned long long)g_walk_fails,
-           (unsigned long long)g_skipv, (unsigned long long)g_skipv_fails, (unsigned long long)fails);
+           (unsigned long long)g_skipv, (unsigned long long)g_skipv_fails, (unsigned long long)g_ff,
+           (unsigned long long)g_ff_steps, (unsigned long long)g_ff_fails, (unsigned long long)fails);
     return fails ? 1 : 0;
 }

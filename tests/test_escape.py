@@ -1,4 +1,5 @@
-"""Host check of the park walk's escape table (csrc/escape.h): on random
+"""Host check of the park walk's escape table and of the primary walk's
+frustum bound (csrc/escape.h): on random
 grids and rays, no cell the cell-by-cell walk (Iterator.next, linalg.zig:478)
 visits after a brick whose escape bit is set for the ray's direction bin
 holds a triangle, so stopping the walk there leaves traceRay's result
@@ -24,7 +25,17 @@ def test_escape_table_is_sound(tmp_path):
                    check=True)
     r = subprocess.run([str(exe), "24", "20000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr + r.stdout
-    res = json.loads(r.stdout)
+    res = {}
+    for line in r.stdout.splitlines():
+        res.update(json.loads(line))
     # the table must actually fire (not vacuously sound) and never be wrong
     assert res["unsound"] == 0 and res["box_fails"] == 0, res
     assert res["escapes"] > 10000 and res["steps_after_escape"] > 100000, res
+    # the primary frustum bound (escape.h frustum_bound lo): no ray of a block
+    # enters an occupied cell below the block's bound, and the bound covers
+    # most of the cells the rays pass
+    assert res["frustum_unsound"] == 0, res
+    assert res["frustum_cells_below_bound"] > 0.3 * res["frustum_steps"], res
+    # the far bound: no occupied cell entered at or past it, and it cuts walks
+    assert res["frustum_far_unsound"] == 0, res
+    assert res["frustum_cells_past_far"] > 0.02 * res["frustum_steps"], res

@@ -497,6 +497,81 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
         (S).pc += k0_ * (S).d0 + k1_ * (S).d1 + k2_ * (S).d2;                                  \
     } while (0)
 
+// Fast-forward of the packed walk through space known to be empty: every
+// Iterator.next step whose crossing t is below TAU, as plain f32 adds per
+// axis (the same adds, in the same order per axis, as the cell-by-cell
+// walk).  The steps are the merge of the three crossing sequences in
+// (t, -axis) order, so the crossings with t < TAU are exactly a prefix of the
+// walk, and the state after them is the walk's state after that many steps.
+// EXITED: one of them was the exit crossing of its axis (Iterator.next
+// returned +inf there; the walk has ended).  The caller guarantees that the
+// cells those steps enter hold no triangle and that nearest > TAU (so no break
+// test fires among them); not used with a -inf/NaN crossing sequence
+// (Dda.neg bit 3).  tests/cpp/dda_skip_check.cpp checks it step for step.
+#define FF_AXIS(S, A, FA, TAU, EXITED)                                                         \
+    while ((S).tn##A < (TAU)) {                                                                \
+        if ((((S).pc ^ (S).pe) & (FA)) == 0u) { (EXITED) = true; break; }                     \
+        (S).tn##A += (S).td##A;                                                                \
+        (S).pc += (S).d##A;                                                                    \
+    }
+#define DDAV_FF(S, F0, F1, F2, TAU, EXITED)                                                    \
+    do {                                                                                       \
+        (EXITED) = false;                                                                      \
+        FF_AXIS(S, 0, F0, TAU, EXITED)                                                         \
+        if (!(EXITED)) { FF_AXIS(S, 1, F1, TAU, EXITED) }                                      \
+        if (!(EXITED)) { FF_AXIS(S, 2, F2, TAU, EXITED) }                                      \
+    } while (0)
+
+// DDAV_FF with four conditional crossings per loop trip and the selects
+// branch-free (fewer exec-mask updates per crossing; same crossings, same
+// state, same EXITED).
+#define FF_AXIS4(S, A, FA, TAU, EXITED)                                                        \
+    for (;;) {                                                                                 \
+        _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                                     \
+            const bool go_ = (S).tn##A < (TAU) && !(EXITED);                                   \
+            const bool at_ = (((S).pc ^ (S).pe) & (FA)) == 0u;                                 \
+            (EXITED) = (EXITED) || (go_ && at_);                                               \
+            const bool mv_ = go_ && !at_;                                                      \
+            (S).tn##A = mv_ ? (S).tn##A + (S).td##A : (S).tn##A;                               \
+            (S).pc = mv_ ? (S).pc + (S).d##A : (S).pc;                                         \
+        }                                                                                      \
+        if (!((S).tn##A < (TAU)) || (EXITED)) break;                                           \
+    }
+#define DDAV_FF4(S, F0, F1, F2, TAU, EXITED)                                                   \
+    do {                                                                                       \
+        (EXITED) = false;                                                                      \
+        FF_AXIS4(S, 0, F0, TAU, EXITED)                                                        \
+        if (!(EXITED)) { FF_AXIS4(S, 1, F1, TAU, EXITED) }                                     \
+        if (!(EXITED)) { FF_AXIS4(S, 2, F2, TAU, EXITED) }                                     \
+    } while (0)
+
+// DDAV_FF for long jumps: per axis first a run of n crossings known to lie
+// below TAU and before the exit cell -- n from a float estimate with a safety
+// margin, capped by the cells left to the exit -- done as n plain adds (the
+// same adds in the same order: the state is the one the cell walk reaches
+// after them) and one packed-cell step of n cells, then FF_AXIS for the last
+// few.  Same crossings, same state, same EXITED as DDAV_FF.
+#define FFC_AXIS(S, A, FA, OA, BA, TAU, EXITED)                                                \
+    {                                                                                          \
+        const float est_ = ((TAU) - (S).tn##A) / (S).td##A;                                    \
+        /* a lower bound on the crossings below TAU: the n adds' rounding drifts by at most */ \
+        /* n TAU 2^-24 <= 6e-5 n td while TAU < 1000 td, inside the 1e-4 n + 2 margin     */ \
+        uint32_t n_ = est_ > 3.0f && (TAU) < 1000.0f * (S).td##A ? (uint32_t)(est_ * 0.9999f) - 2u : 0u; \
+        const uint32_t c_ = ZRT_UBFE((S).pc, (OA), (BA)), e_ = ZRT_UBFE((S).pe, (OA), (BA));  \
+        const uint32_t left_ = c_ > e_ ? c_ - e_ : e_ - c_;   /* cells before the exit one */  \
+        n_ = zmin(n_, left_);                                                                  \
+        for (uint32_t k_ = 0; k_ < n_; ++k_) (S).tn##A += (S).td##A;                           \
+        (S).pc += n_ * (S).d##A;                                                               \
+    }                                                                                          \
+    FF_AXIS(S, A, FA, TAU, EXITED)
+#define DDAV_FFC(S, K, F0, F1, F2, TAU, EXITED)                                                \
+    do {                                                                                       \
+        (EXITED) = false;                                                                      \
+        FFC_AXIS(S, 0, F0, 0u, (K).b0, TAU, EXITED)                                            \
+        if (!(EXITED)) { FFC_AXIS(S, 1, F1, (K).o1, (K).b1, TAU, EXITED) }                     \
+        if (!(EXITED)) { FFC_AXIS(S, 2, F2, (K).o2, (K).b2, TAU, EXITED) }                     \
+    } while (0)
+
 // Select of the park kernel's pair refill (render.hip): position of the r-th
 // (from 0) set bit of m, r < popcount(m).  The byte holding it comes from
 // three prefix popcounts, its position within the byte from a 2 KB LDS table

@@ -118,4 +118,98 @@ ZHD bool esc_compute(const EscSat& S, const uint32_t res[3], const float cs[3], 
     return true;
 }
 
+// Primary-ray frustum bound (the primary launch, render.hip frustum_kernel).
+// Every camera ray of the pixel block [u0, u1) x [v0, v1) (pixel x + jitter,
+// stage3.zig:234-238) starts at the camera origin o with direction
+// normalize(llc + right u + up v): the points o + s D(u, v), s >= 0, form a
+// cone over the parallelogram of D's, and its slice s in [s0, s1] is the
+// convex hull of the eight corner points.  Marching slices of about two cells
+// along the cone's dominant axis, the first slice whose box (dilated by one
+// cell) holds an occupied cell ends the march: every point of the block's
+// rays with normalized t < s0 |D|min lies in earlier, empty slices, so a walk
+// may fast-forward (DDAV_FF) over every crossing below that t.  +inf: the cone
+// meets no occupied cell at all, so every ray of the block misses
+// (traceRay's +inf).  0: no bound (a degenerate cone).
+// hi: the march goes on to the last slice [s0, s1] that holds an occupied
+// cell: every point of the block's rays with t >= s1 |D|max lies in later,
+// empty slices, so once the walk has tested a cell whose exit crossing is at
+// or past hi no later cell can change the result (+inf: no bound).
+struct FrustumBound {
+    float lo, hi;
+};
+ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const float bmin[3], const float bmax[3],
+                               const float cs[3], const float org[3], const float llc[3], const float right[3],
+                               const float up[3], double u0, double u1, double v0, double v1) {
+    FrustumBound fb{0.0f, kInf};
+    double D[4][3];
+    const double uu[2] = {u0, u1}, vv[2] = {v0, v1};
+    double dmin = 1e300, dmax = 0.0, mid[3] = {0, 0, 0};
+    for (int c = 0; c < 4; ++c) {
+        double n2 = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            D[c][k] = (double)llc[k] + (double)right[k] * uu[c & 1] + (double)up[k] * vv[c >> 1];
+            n2 += D[c][k] * D[c][k];
+            mid[k] += 0.25 * D[c][k];
+        }
+        dmin = fmin(dmin, sqrt(n2));
+        dmax = fmax(dmax, sqrt(n2));
+    }
+    // |D| over the parallelogram >= the corners' least |D| minus its diagonals
+    double rl = 0.0, ul = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        rl += (double)right[k] * right[k];
+        ul += (double)up[k] * up[k];
+    }
+    dmin -= sqrt(rl) * (u1 - u0) + sqrt(ul) * (v1 - v0);
+    if (!(dmin > 0.0)) return fb;
+    // beyond s_far every point of the cone is farther from o than any grid point
+    double far2 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double a = fabs((double)bmin[k] - org[k]), b = fabs((double)bmax[k] - org[k]);
+        far2 += fmax(a, b) * fmax(a, b);
+    }
+    const double s_far = sqrt(far2) / dmin;
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (fabs(mid[k]) / cs[k] > fabs(mid[ax]) / cs[ax]) ax = k;
+    const double ds = 2.0 * (double)cs[ax] / fmax(fabs(mid[ax]), 1e-30);
+    if (!(ds > 0.0)) return fb;
+    double first = -1.0, last = -1.0;
+    for (int it = 0; it < 1 << 16; ++it) {
+        const double s0 = it * ds, s1 = s0 + ds;
+        if (s0 > s_far) break;
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int c = 0; c < 4; ++c)
+            for (int k = 0; k < 3; ++k) {
+                const double p0 = org[k] + s0 * D[c][k], p1 = org[k] + s1 * D[c][k];
+                lo[k] = fmin(lo[k], fmin(p0, p1));
+                hi[k] = fmax(hi[k], fmax(p0, p1));
+            }
+        uint32_t c0[3], c1[3];
+        bool outside = false;
+        for (int k = 0; k < 3; ++k) {
+            const double a = floor((lo[k] - bmin[k]) / cs[k]) - 1.0, b = floor((hi[k] - bmin[k]) / cs[k]) + 1.0;
+            if (b < 0.0 || a > res[k] - 1.0) { outside = true; break; }
+            c0[k] = (uint32_t)fmax(0.0, a);
+            c1[k] = (uint32_t)fmin(res[k] - 1.0, b);
+        }
+        if (outside) continue;
+        if (esc_box(S, c0[0], c1[0], c0[1], c1[1], c0[2], c1[2]) != 0u) {
+            if (first < 0.0) first = s0;
+            last = s1;
+        }
+    }
+    if (!(s_far * 0.0 == 0.0) || (double)(1 << 16) * ds <= s_far) return fb;   // the march did not reach s_far
+    if (first < 0.0) {
+        fb.lo = kInf;
+        return fb;
+    }
+    const double tl = first * dmin, th = last * dmax;
+    fb.lo = (float)tl;
+    if ((double)fb.lo > tl) fb.lo = nextafterf(fb.lo, 0.0f);     // round down
+    fb.hi = (float)th;
+    if ((double)fb.hi < th) fb.hi = nextafterf(fb.hi, kInf);     // round up
+    return fb;
+}
+
 }  // namespace zrt

@@ -95,6 +95,19 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_ESC_NODMA
 #define ZRT_ESC_NODMA 0
 #endif
+// ZRT_FRUSTUM: the primary walk fast-forwards (DDAV_FF) over the crossings
+// below its pixel block's frustum bound (escape.h frustum_bound lo); with
+// ZRT_FRUSTUM_HI it also stops once it has tested the cell whose exit is at
+// or past the block's far bound (hi)
+#ifndef ZRT_FRUSTUM
+#define ZRT_FRUSTUM 1
+#endif
+#ifndef ZRT_FRUSTUM_HI
+#define ZRT_FRUSTUM_HI 1
+#endif
+#ifndef ZRT_FF4
+#define ZRT_FF4 0
+#endif
 // ZRT_PARK_MISS: a bounce segment that misses ends in the park kernel
 // (terminal radiance = the sky colour, stage3.zig:195-197), so the shade
 // kernel loads the path records of hits only
@@ -130,6 +143,11 @@ struct TraceParams {
     const double* zig;        // zx[257], zf[257]
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
+    // primary launch: per 8x8 pixel block of the image (row-major, tlo_nbx
+    // blocks per row) the frustum bounds (lo, hi) of escape.h frustum_bound,
+    // or null
+    const float2* tlo;
+    uint32_t tlo_nbx;
     // packed walks (DdaV): the layout, the cells indexed by the packed word
     // (the cells themselves for power-of-two grids, else a padded copy), the
     // coarse-brick fields of the packed word (offset, width per axis) and
@@ -269,10 +287,14 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // PACKED: the walk state with the cell packed into one word (DdaV, grids of
 // at most 1024 cells per axis; same cells, same order, same t_exit), which
 // also indexes the cell records (cell32).
+// TAU (packed walk): a frustum bound (escape.h frustum_bound lo) for this ray: the
+// crossings below it enter only empty cells; +inf: the ray meets no
+// occupied cell at all.
 template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
-                                           uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr) {
+                                           uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr,
+                                           float tau = 0.0f, float tfar = kInf) {
     float nearest = kInf;
     Dda s0;
     if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
@@ -288,12 +310,29 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // every step (r03 ISA)
         uint32_t f0 = p.pk.f0, f1 = p.pk.f1, f2 = p.pk.f2;
         asm("" : "+s"(f0), "+s"(f1), "+s"(f2));
+        if (ZRT_FRUSTUM && s0.neg < 8u) {
+            // the cells before tau are empty (the pixel block's frustum bound):
+            // their crossings as plain adds, the walk's exact state after them
+            // (DDAV_FF); nearest is +inf here, so no break test fires among them
+            if (tau == kInf) return nearest;               // no occupied cell on the ray: the miss
+            if (tau > fminf(s.tn0, fminf(s.tn1, s.tn2))) {
+                bool exited;
+                if (ZRT_FF4 == 2) DDAV_FFC(s, p.pk, f0, f1, f2, tau, exited);
+                else if (ZRT_FF4) DDAV_FF4(s, f0, f1, f2, tau, exited);
+                else DDAV_FF(s, f0, f1, f2, tau, exited);
+                if (exited) return nearest;
+            }
+        }
         bool occupied = brick_occupied_v(p, occ, s.pc);
         const bool skip_ok = ZRT_PRIM_SKIP && s0.neg < 8u;
+        // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
+        // bound) the t past which every cell of the ray is empty
+        float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
                 test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+                lim = fminf(lim, nearest);                 // = min(nearest, far bound)
             }
             bool crossed, exited;
             float tc;
@@ -307,7 +346,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             } else {
                 DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             }
-            if (exited || nearest <= tc) break;            // stage3.zig:179-182 (T_EXIT = +inf at the exit)
+            if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
         return nearest;
@@ -395,12 +434,14 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // pass item `item` (= packed pixel * S + s_local: pixel-major, so one
 // pixel's samples are consecutive items and a wave's records are
 // contiguous); leaves rng after the jitter.
-__device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, Rng& rng, v3& o, v3& d) {
+__device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, Rng& rng, v3& o, v3& d,
+                                           uint32_t* block = nullptr) {
     const uint32_t q = div_by(item, p.sdiv);
     const uint32_t s_local = item - q * p.S;
     const uint32_t pixel = p.pixlist[q];
     const uint32_t py = pixel / p.w;
     const uint32_t px = pixel - py * p.w;
+    if (block) *block = (py >> 3) * p.tlo_nbx + (px >> 3);
     rng.s = path_key(p.seed, pixel, p.s0 + s_local);
     const float jx = rng_float(rng);
     const float jy = rng_float(rng);
@@ -775,9 +816,16 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             // mask) is re-read after the walk, so it holds no VGPRs in it
             v3 o, d;
             uint32_t depth;
+            float tau = 0.0f, tfar = kInf;
             if (PRIMARY) {
                 Rng rng0;
-                camera_ray(p, i, rng0, o, d);
+                uint32_t blk = 0;
+                camera_ray(p, i, rng0, o, d, &blk);
+                if (ZRT_FRUSTUM && p.tlo) {
+                    const float2 fb = p.tlo[blk];
+                    tau = fb.x;
+                    tfar = fb.y;
+                }
                 depth = p.max_bounce;
             } else {
                 const float4 a = w.q_in[3ull * i], b = w.q_in[3ull * i + 1];
@@ -789,7 +837,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             uint32_t hidx = 0;
             WF_STAMP(2);
             if (depth != 0)
-                t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr);
+                t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
+                                                        tau, tfar);
             WF_STAMP(0);
             uint32_t item, slot;
             Rng rng;
@@ -1717,6 +1766,9 @@ struct zrt_context {
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
     uint32_t* d_esc = nullptr;      // escape table (escape.h), with OccX
+    uint32_t* d_sat = nullptr;      // summed-area table of cell occupancy (escape.h EscSat), or null
+    // the primary frustum bounds (frustum_kernel) per 8x8 pixel block
+    float2* d_tlo = nullptr; size_t tlo_cap = 0;
     bool esc_on = false;            // the park launches use it (dense enough to pay, context_escape)
     double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
@@ -1836,6 +1888,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     DeviceGuard g(c->device);
     if (c->d_cell32) (void)hipFree(c->d_cell32);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_esc,
+                    c->d_sat, c->d_tlo,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2189,29 +2242,53 @@ constexpr double kEscMinDensity = 0.12;
 // The escape table for a context with OccX (the park walk); none for grids
 // whose summed-area table would pass 2^28 entries (the walk then never stops
 // early, as before).
-static int context_escape(zrt_context* c) {
-    if (!ZRT_ESCAPE || !c->occx_ok) return ZRT_OK;
+// Primary frustum bounds (escape.h frustum_bound): one thread per 8x8 pixel
+// block of the w x h image.
+struct FrustumArgs {
+    uint32_t res[3];
+    float bmin[3], bmax[3], cs[3], org[3], llc[3], right[3], up[3];
+    uint32_t w, h, nbx, nby;
+};
+__global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
+                                                         float2* __restrict__ tlo) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= a.nbx * a.nby) return;
+    const uint32_t bx = b % a.nbx, by = b / a.nbx;
+    const EscSat S{sat, a.res[0] + 1u, (a.res[0] + 1u) * (a.res[1] + 1u)};
+    const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx,
+                                          8.0 * bx + 8.0, 8.0 * by, 8.0 * by + 8.0);
+    tlo[b] = make_float2(fb.lo, fb.hi);
+}
+
+// The summed-area table of cell occupancy (escape.h EscSat): kept in the
+// context for the escape table and the primary frustum bounds; none for grids
+// whose table would pass 2^28 entries (1 GiB).
+static int context_sat(zrt_context* c) {
     const uint32_t* r = c->grid.resolution;
     const uint64_t n0 = r[0] + 1ull, n1 = r[1] + 1ull, n2 = r[2] + 1ull;
     if (n0 * n1 * n2 > (1ull << 28)) return ZRT_OK;
-    const uint64_t nbr = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
-    struct Scratch {
-        uint32_t* sat = nullptr;
-        ~Scratch() { if (sat) (void)hipFree(sat); }
-    } tmp;
-    HIP_TRY(hipMalloc((void**)&tmp.sat, 4ull * n0 * n1 * n2));
-    HIP_TRY(hipMalloc((void**)&c->d_esc, 4ull * kEscWords * nbr));
-    HIP_TRY(hipMemsetAsync(tmp.sat, 0, 4ull * n0 * n1 * n2, c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_esc, 0, 4ull * kEscWords * nbr, c->stream));
+    HIP_TRY(hipMalloc((void**)&c->d_sat, 4ull * n0 * n1 * n2));
+    HIP_TRY(hipMemsetAsync(c->d_sat, 0, 4ull * n0 * n1 * n2, c->stream));
     hipLaunchKernelGGL(esc_sat_fill_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1], c->ncells,
-                       (uint32_t)n0, (uint32_t)(n0 * n1), tmp.sat);
+                       (uint32_t)n0, (uint32_t)(n0 * n1), c->d_sat);
     const uint64_t lines[3] = {n1 * n2, n0 * n2, n0 * n1};
     for (uint32_t a = 0; a < 3; ++a)
         hipLaunchKernelGGL(esc_sat_scan_kernel, dim3((uint32_t)((lines[a] + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           c->stream, tmp.sat, (uint32_t)n0, (uint32_t)n1, (uint32_t)n2, a);
+                           c->stream, c->d_sat, (uint32_t)n0, (uint32_t)n1, (uint32_t)n2, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ZRT_OK;
+}
+
+static int context_escape(zrt_context* c) {
+    if (!ZRT_ESCAPE || !c->occx_ok || !c->d_sat) return ZRT_OK;
+    const uint32_t* r = c->grid.resolution;
+    const uint64_t nbr = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
+    HIP_TRY(hipMalloc((void**)&c->d_esc, 4ull * kEscWords * nbr));
+    HIP_TRY(hipMemsetAsync(c->d_esc, 0, 4ull * kEscWords * nbr, c->stream));
     const uint64_t nthr = nbr * kEscNBin;
     hipLaunchKernelGGL(esc_build_kernel, dim3((uint32_t)((nthr + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                       (const uint32_t*)tmp.sat, r[0], r[1], r[2], c->grid.cell_size[0], c->grid.cell_size[1],
+                       (const uint32_t*)c->d_sat, r[0], r[1], r[2], c->grid.cell_size[0], c->grid.cell_size[1],
                        c->grid.cell_size[2], c->occx_nb[0], c->occx_nb[1], (uint32_t)nbr, c->d_esc);
     HIP_TRY(hipGetLastError());
     // Use it when enough of its bits are set: each walk trip of the park
@@ -2265,6 +2342,8 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
         if (!occx_possible) {
             c->occx_ok = false;
+            const int rc = context_sat(c);
+            if (rc != ZRT_OK) return rc;
             return context_counters(c);
         }
         std::vector<uint32_t> bits(nbw, 0u);
@@ -2346,7 +2425,8 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         c->occx_nbw = (uint32_t)nbw;
         c->occx_moff = (uint32_t)moff;
     }
-    int rc = context_escape(c);
+    int rc = context_sat(c);
+    if (rc == ZRT_OK) rc = context_escape(c);
     if (rc != ZRT_OK) return rc;
     return context_counters(c);
 }
@@ -2802,6 +2882,29 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 512, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
+    if (ZRT_FRUSTUM && c->d_sat && !counting && packed) {
+        // the primary frustum bounds of this camera, every render (inside the
+        // timed region: 32 K threads for a 1080p frame)
+        const uint32_t nbx = (cam->w + 7u) / 8u, nby = (cam->h + 7u) / 8u;
+        if ((rc = grow(&c->d_tlo, &c->tlo_cap, (size_t)nbx * nby)) != ZRT_OK) return rc;
+        FrustumArgs fa;
+        for (int k = 0; k < 3; ++k) {
+            fa.res[k] = c->grid.resolution[k];
+            fa.bmin[k] = c->grid.bbox_min[k];
+            fa.bmax[k] = c->grid.bbox_max[k];
+            fa.cs[k] = c->grid.cell_size[k];
+            fa.org[k] = cam->origin[k];
+            fa.llc[k] = cam->lower_left_corner[k];
+            fa.right[k] = cam->right[k];
+            fa.up[k] = cam->up[k];
+        }
+        fa.w = cam->w; fa.h = cam->h; fa.nbx = nbx; fa.nby = nby;
+        hipLaunchKernelGGL(frustum_kernel, dim3((nbx * nby + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                           (const uint32_t*)c->d_sat, fa, c->d_tlo);
+        HIP_TRY(hipGetLastError());
+        tp.tlo = c->d_tlo;
+        tp.tlo_nbx = nbx;
+    }
     if (nsets > 1) {                           // the other sets start after the stats reset
         HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
         for (uint32_t k = 1; k < nsets; ++k) HIP_TRY(hipStreamWaitEvent(c->set[k].stream, c->ev_fork, 0));
