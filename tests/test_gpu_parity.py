@@ -319,6 +319,46 @@ def test_render_max_bounce_variants(oracle_mod, gpu_scenes, mode, flags, mb):
     assert np.array_equal(img.reshape(-1, 3), rgb)
 
 
+def _look_camera(org, tgt, fov, w, h):
+    f = tgt - org
+    f /= np.linalg.norm(f)
+    rt = np.cross(f, [0.3, 1.0, 0.2])
+    rt /= np.linalg.norm(rt)
+    up = np.cross(rt, f)
+    px = 2.0 * np.tan(0.5 * fov) / h
+    cam = native.Camera()
+    cam.w, cam.h = w, h
+    llc = f - rt * px * 0.5 * w - up * px * 0.5 * h
+    for k in range(3):
+        cam.origin[k], cam.lower_left_corner[k] = float(org[k]), float(llc[k])
+        cam.right[k], cam.up[k] = float(rt[k] * px), float(up[k] * px)
+    return cam
+
+
+@pytest.mark.parametrize("name", ["contest", "sponza", "cornell"])
+def test_frustum_bounds_random_cameras_identical(gpu_scenes, name):
+    """The primary launch's frustum bounds (escape.h frustum_bound: the
+    fast-forward below lo, the stop past hi, the +inf blocks) against the
+    counting build, which walks every cell: random cameras inside and outside
+    the grid, wide and narrow, image sizes not multiples of the 8x8 block."""
+    soup = scenes.get_scene(name)
+    p = np.asarray(soup.pos, np.float64).reshape(-1, 3)
+    lo, hi = p.min(0), p.max(0)
+    ext = hi - lo
+    rng = np.random.default_rng(7)
+    rs = gpu_scenes(name)
+    for k in range(6):
+        inside = k % 2 == 0
+        org = lo + ext * (rng.random(3) if inside else -1.0 + 3.0 * rng.random(3))
+        tgt = lo + ext * rng.random(3)
+        cam = _look_camera(org, tgt, rng.uniform(0.2, 1.6), 36 + 4 * k, 29 + 3 * k)
+        ref, r0 = rs.render(cam, num_samples=3, max_bounce=2, stats=True, linear=True)
+        img, r1 = rs.render(cam, num_samples=3, max_bounce=2, linear=True)
+        assert np.array_equal(ref, img), (k, inside)
+        assert np.array_equal(r0["linear"], r1["linear"]), k
+        assert r0["stats"]["segments"] == r1["stats"]["segments"], k
+
+
 def test_render_seed_changes_image(gpu_scenes):
     soup = scenes.get_scene("sphere")
     cam = camera_for(soup, None, 32, 32)
