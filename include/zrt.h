@@ -102,7 +102,7 @@ typedef struct zrt_render_config {
     int32_t device;                  /* HIP ordinal, -1 = current device */
     uint32_t rank;                   /* this process's shard of the image */
     uint32_t num_ranks;              /* tiles t with t % num_ranks == rank */
-    uint32_t tile_size;              /* square tile edge in pixels, 0 = 64 */
+    uint32_t tile_size;              /* square tile edge in pixels, 0 = 64 (32 over several devices) */
     uint32_t flags;                  /* ZRT_FLAG_* */
     uint32_t samples_per_pass;       /* samples of every pixel per device pass, 0 = automatic: as few
                                         passes as 144 GiB of path queues allow, at least two for frames
