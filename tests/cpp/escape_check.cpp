@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
     // before it (a +inf bound: the ray enters no occupied cell at all), nor
     // at a crossing at or past its hi bound
     uint64_t f_rays = 0, f_skipped = 0, f_steps = 0, f_unsound = 0, f_miss_blocks = 0, f_blocks = 0;
-    uint64_t f_far = 0, f_far_unsound = 0;
+    uint64_t f_far = 0, f_far_unsound = 0, f_gap = 0, f_gap_unsound = 0, f_gap_blocks = 0;
     for (int gi = 0; gi < n_grids; ++gi) {
         uint32_t res[3];
         float bmin[3], bmax[3], cs[3];
@@ -184,7 +184,8 @@ int main(int argc, char** argv) {
                 for (uint32_t bx = 0; bx < W / 8; ++bx) {
                     const FrustumBound fb = frustum_bound(S, res, bmin, bmax, cs, org, llc_, right_, up_, 8.0 * bx,
                                                           8.0 * bx + 8.0, 8.0 * by, 8.0 * by + 8.0);
-                    const float tlo = fb.lo, thi = fb.hi;
+                    const float tlo = fb.lo, thi = fb.hi, ga = fb.ga, gb = fb.gb;
+                    f_gap_blocks += ga < gb;
                     ++f_blocks;
                     f_miss_blocks += tlo == kInf;
                     for (int r = 0; r < 40; ++r) {
@@ -213,6 +214,10 @@ int main(int argc, char** argv) {
                                 ++f_far;
                                 if (o_) { ++f_far_unsound; break; }
                             }
+                            if (guard > 0 && tin >= ga && tin < gb) {   // entered inside the gap
+                                ++f_gap;
+                                if (o_) { ++f_gap_unsound; break; }
+                            }
                             bool crossed;
                             float te;
                             const float tc = fminf(s.tn0, fminf(s.tn1, s.tn2));
@@ -227,11 +232,13 @@ int main(int argc, char** argv) {
     }
     printf("{\"frustum_blocks\": %llu, \"frustum_miss_blocks\": %llu, \"frustum_rays\": %llu, \"frustum_steps\": %llu, "
            "\"frustum_cells_below_bound\": %llu, \"frustum_unsound\": %llu, \"frustum_cells_past_far\": %llu, "
-           "\"frustum_far_unsound\": %llu}\n",
+           "\"frustum_far_unsound\": %llu, \"frustum_gap_blocks\": %llu, \"frustum_cells_in_gap\": %llu, "
+           "\"frustum_gap_unsound\": %llu}\n",
            (unsigned long long)f_blocks, (unsigned long long)f_miss_blocks, (unsigned long long)f_rays,
            (unsigned long long)f_steps, (unsigned long long)f_skipped, (unsigned long long)f_unsound,
-           (unsigned long long)f_far, (unsigned long long)f_far_unsound);
-    unsound += f_unsound + f_far_unsound;
+           (unsigned long long)f_far, (unsigned long long)f_far_unsound, (unsigned long long)f_gap_blocks,
+           (unsigned long long)f_gap, (unsigned long long)f_gap_unsound);
+    unsound += f_unsound + f_far_unsound + f_gap_unsound;
     printf("{\"rays\": %llu, \"steps\": %llu, \"escapes\": %llu, \"steps_after_escape\": %llu, \"bits_set\": %.4f, "
            "\"unsound\": %llu, \"box_fails\": %llu}\n",
            (unsigned long long)rays, (unsigned long long)steps, (unsigned long long)escapes,

@@ -39,3 +39,6 @@ def test_escape_table_is_sound(tmp_path):
     # the far bound: no occupied cell entered at or past it, and it cuts walks
     assert res["frustum_far_unsound"] == 0, res
     assert res["frustum_cells_past_far"] > 0.02 * res["frustum_steps"], res
+    # the gap: no occupied cell entered inside it, and it holds cells
+    assert res["frustum_gap_unsound"] == 0, res
+    assert res["frustum_gap_blocks"] > 20 and res["frustum_cells_in_gap"] > 5000, res

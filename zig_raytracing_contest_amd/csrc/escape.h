@@ -134,13 +134,19 @@ ZHD bool esc_compute(const EscSat& S, const uint32_t res[3], const float cs[3], 
 // cell: every point of the block's rays with t >= s1 |D|max lies in later,
 // empty slices, so once the walk has tested a cell whose exit crossing is at
 // or past hi no later cell can change the result (+inf: no bound).
+// [ga, gb]: the longest run of at least kFrustumGapSlices empty slices
+// between occupied ones, as t: every point of the block's rays with t in
+// [ga, gb] lies in it (ga = s_start |D|max rounded up, gb = s_end |D|min
+// rounded down), so a walk that enters a cell at a crossing in [ga, gb) may
+// fast-forward over every crossing below gb (+inf, +inf: no gap).
+constexpr int kFrustumGapSlices = 2;
 struct FrustumBound {
-    float lo, hi;
+    float lo, hi, ga, gb;
 };
 ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const float bmin[3], const float bmax[3],
                                const float cs[3], const float org[3], const float llc[3], const float right[3],
                                const float up[3], double u0, double u1, double v0, double v1) {
-    FrustumBound fb{0.0f, kInf};
+    FrustumBound fb{0.0f, kInf, kInf, kInf};
     double D[4][3];
     const double uu[2] = {u0, u1}, vv[2] = {v0, v1};
     double dmin = 1e300, dmax = 0.0, mid[3] = {0, 0, 0};
@@ -174,7 +180,8 @@ ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const flo
         if (fabs(mid[k]) / cs[k] > fabs(mid[ax]) / cs[ax]) ax = k;
     const double ds = 2.0 * (double)cs[ax] / fmax(fabs(mid[ax]), 1e-30);
     if (!(ds > 0.0)) return fb;
-    double first = -1.0, last = -1.0;
+    double first = -1.0, last = -1.0, gap_s = -1.0, best0 = 0.0, best1 = 0.0, best_len = -1.0;
+    int run = 0;
     for (int it = 0; it < 1 << 16; ++it) {
         const double s0 = it * ds, s1 = s0 + ds;
         if (s0 > s_far) break;
@@ -193,10 +200,18 @@ ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const flo
             c0[k] = (uint32_t)fmax(0.0, a);
             c1[k] = (uint32_t)fmin(res[k] - 1.0, b);
         }
-        if (outside) continue;
-        if (esc_box(S, c0[0], c1[0], c0[1], c1[1], c0[2], c1[2]) != 0u) {
+        if (!outside && esc_box(S, c0[0], c1[0], c0[1], c1[1], c0[2], c1[2]) != 0u) {
+            if (first >= 0.0 && run >= kFrustumGapSlices && (s0 * dmin - gap_s * dmax) > best_len) {
+                best_len = s0 * dmin - gap_s * dmax;
+                best0 = gap_s;
+                best1 = s0;
+            }
             if (first < 0.0) first = s0;
             last = s1;
+            run = 0;
+        } else {
+            if (run == 0) gap_s = s0;
+            ++run;
         }
     }
     if (!(s_far * 0.0 == 0.0) || (double)(1 << 16) * ds <= s_far) return fb;   // the march did not reach s_far
@@ -209,6 +224,16 @@ ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const flo
     if ((double)fb.lo > tl) fb.lo = nextafterf(fb.lo, 0.0f);     // round down
     fb.hi = (float)th;
     if ((double)fb.hi < th) fb.hi = nextafterf(fb.hi, kInf);     // round up
+    if (best_len > 0.0) {
+        const double ta = best0 * dmax, tb = best1 * dmin;
+        float ga = (float)ta, gb = (float)tb;
+        if ((double)ga < ta) ga = nextafterf(ga, kInf);          // round up
+        if ((double)gb > tb) gb = nextafterf(gb, 0.0f);          // round down
+        if (ga < gb) {
+            fb.ga = ga;
+            fb.gb = gb;
+        }
+    }
     return fb;
 }
 

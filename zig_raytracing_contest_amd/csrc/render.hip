@@ -105,6 +105,11 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_FRUSTUM_HI
 #define ZRT_FRUSTUM_HI 1
 #endif
+// ZRT_FRUSTUM_GAP: a walk entering a cell inside the block's empty gap
+// (escape.h frustum_bound ga, gb) fast-forwards to gb
+#ifndef ZRT_FRUSTUM_GAP
+#define ZRT_FRUSTUM_GAP 1
+#endif
 // ZRT_FF4: the fast-forward as DDAV_FF4 (four branch-free crossings per loop
 // trip; r04s, full spp: cfg3 5730 vs 5695 Mrays/s with DDAV_FF, 5419 without
 // the bounds; cfg5 and cfg2 equal), 2: DDAV_FFC, 0: DDAV_FF
@@ -147,9 +152,9 @@ struct TraceParams {
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
     // primary launch: per 8x8 pixel block of the image (row-major, tlo_nbx
-    // blocks per row) the frustum bounds (lo, hi) of escape.h frustum_bound,
-    // or null
-    const float2* tlo;
+    // blocks per row) the frustum bounds (lo, hi, ga, gb) of escape.h
+    // frustum_bound, or null
+    const float4* tlo;
     uint32_t tlo_nbx;
     // packed walks (DdaV): the layout, the cells indexed by the packed word
     // (the cells themselves for power-of-two grids, else a padded copy), the
@@ -297,7 +302,8 @@ template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr,
-                                           float tau = 0.0f, float tfar = kInf) {
+                                           float tau = 0.0f, float tfar = kInf, float ga = kInf,
+                                           float gb = kInf) {
     float nearest = kInf;
     Dda s0;
     if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
@@ -331,6 +337,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
         // bound) the t past which every cell of the ray is empty
         float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
+        if (s0.neg >= 8u) ga = kInf;                       // (the gap fast-forward: see below)
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
@@ -350,6 +357,19 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                 DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             }
             if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
+            if (ZRT_FRUSTUM_GAP && tc >= ga) {
+                // the cell just entered lies in the block's empty gap: the
+                // crossings below gb enter empty cells, and with lim >= gb no
+                // stop test fires among them (the walk's state after them)
+                ga = kInf;
+                if (lim >= gb) {
+                    if (ZRT_FF4 == 2) DDAV_FFC(s, p.pk, f0, f1, f2, gb, exited);
+                    else if (ZRT_FF4) DDAV_FF4(s, f0, f1, f2, gb, exited);
+                    else DDAV_FF(s, f0, f1, f2, gb, exited);
+                    if (exited) break;
+                    crossed = true;
+                }
+            }
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
         return nearest;
@@ -819,15 +839,17 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             // mask) is re-read after the walk, so it holds no VGPRs in it
             v3 o, d;
             uint32_t depth;
-            float tau = 0.0f, tfar = kInf;
+            float tau = 0.0f, tfar = kInf, ga = kInf, gb = kInf;
             if (PRIMARY) {
                 Rng rng0;
                 uint32_t blk = 0;
                 camera_ray(p, i, rng0, o, d, &blk);
                 if (ZRT_FRUSTUM && p.tlo) {
-                    const float2 fb = p.tlo[blk];
+                    const float4 fb = p.tlo[blk];
                     tau = fb.x;
                     tfar = fb.y;
+                    ga = fb.z;
+                    gb = fb.w;
                 }
                 depth = p.max_bounce;
             } else {
@@ -841,7 +863,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             WF_STAMP(2);
             if (depth != 0)
                 t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
-                                                        tau, tfar);
+                                                        tau, tfar, ga, gb);
             WF_STAMP(0);
             uint32_t item, slot;
             Rng rng;
@@ -1771,7 +1793,7 @@ struct zrt_context {
     uint32_t* d_esc = nullptr;      // escape table (escape.h), with OccX
     uint32_t* d_sat = nullptr;      // summed-area table of cell occupancy (escape.h EscSat), or null
     // the primary frustum bounds (frustum_kernel) per 8x8 pixel block
-    float2* d_tlo = nullptr; size_t tlo_cap = 0;
+    float4* d_tlo = nullptr; size_t tlo_cap = 0;
     bool esc_on = false;            // the park launches use it (dense enough to pay, context_escape)
     double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
@@ -2253,14 +2275,14 @@ struct FrustumArgs {
     uint32_t w, h, nbx, nby;
 };
 __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
-                                                         float2* __restrict__ tlo) {
+                                                         float4* __restrict__ tlo) {
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= a.nbx * a.nby) return;
     const uint32_t bx = b % a.nbx, by = b / a.nbx;
     const EscSat S{sat, a.res[0] + 1u, (a.res[0] + 1u) * (a.res[1] + 1u)};
     const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx,
                                           8.0 * bx + 8.0, 8.0 * by, 8.0 * by + 8.0);
-    tlo[b] = make_float2(fb.lo, fb.hi);
+    tlo[b] = make_float4(fb.lo, fb.hi, fb.ga, fb.gb);
 }
 
 // The summed-area table of cell occupancy (escape.h EscSat): kept in the
