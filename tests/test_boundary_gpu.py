@@ -98,6 +98,7 @@ def test_group_built_and_rank_share():
     finally:
         grp.close()
     mine = native.tile_pixels(cam.w, cam.h, 32, 1, 2)       # 32x32 tiles: the default over several devices
+    assert 0 < mine.size < cam.w * cam.h
     flat = part.reshape(-1, 3)
     assert np.array_equal(flat[mine], g["rgb"][mine])
     other = np.ones(cam.w * cam.h, bool)

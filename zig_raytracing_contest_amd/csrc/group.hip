@@ -190,7 +190,9 @@ extern "C" int zrt_group_render(zrt_group* g, const zrt_camera* cam, const zrt_r
             th.emplace_back([&, i] {
                 zrt_render_config c = *cfg;
                 c.device = g->devices[i];
-                c.rank = cfg->rank * n + i;    // device i takes sub-rank i of this process's share
+                // device i takes the i-th of every n of this process's tiles
+                // (t % nr == rank, (t / nr) % n == i): t % (nr n) == rank + nr i
+                c.rank = cfg->rank + nr * i;
                 c.num_ranks = nr * n;
                 c.tile_size = tile;
                 c.num_devices = 0;
