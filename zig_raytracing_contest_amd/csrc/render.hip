@@ -106,9 +106,10 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #define ZRT_FRUSTUM_HI 1
 #endif
 // ZRT_FRUSTUM_GAP: a walk entering a cell inside the block's empty gap
-// (escape.h frustum_bound ga, gb) fast-forwards to gb
+// (escape.h frustum_bound ga, gb) fast-forwards to gb (r04v: neutral, cfg3
+// 5756 vs 5756 Mrays/s, cfg5 / cfg2 within noise; off)
 #ifndef ZRT_FRUSTUM_GAP
-#define ZRT_FRUSTUM_GAP 1
+#define ZRT_FRUSTUM_GAP 0
 #endif
 // ZRT_FF4: the fast-forward as DDAV_FF4 (four branch-free crossings per loop
 // trip; r04s, full spp: cfg3 5730 vs 5695 Mrays/s with DDAV_FF, 5419 without
