@@ -2190,7 +2190,13 @@ static uint64_t occx_lds_words(uint64_t nbw, uint64_t moff, uint64_t words) {
 //    the bits take at most kOccLdsMax bytes, coarser bricks (8^3, 16^3, ...:
 //    OR of the 4^3 ones) for larger grids -- result-invariant, an empty brick
 //    only lets the walk skip the range loads of its cells.
-constexpr uint64_t kOccLdsMax = 16 << 10;
+#ifndef ZRT_OCC_LDS_KB
+#define ZRT_OCC_LDS_KB 16
+#endif
+#ifndef ZRT_OCC_SH0
+#define ZRT_OCC_SH0 2
+#endif
+constexpr uint64_t kOccLdsMax = (uint64_t)ZRT_OCC_LDS_KB << 10;
 
 __global__ __launch_bounds__(kBlock) void occ_coarsen_kernel(const uint32_t* __restrict__ bits4, uint32_t nb0,
                                                              uint32_t nb1, uint32_t nb, uint32_t dsh, uint32_t cn0,
@@ -2340,7 +2346,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     // indices), the bounces take the lane walk over the coarse bits below
     const bool occx_possible = occx_usable(nb, 0, 0, 1);
     const uint64_t nbw = (nb + 31) / 32;
-    uint32_t sh = 2;
+    uint32_t sh = ZRT_OCC_SH0;
     auto words_at = [&](uint32_t k) {
         const uint64_t n = (uint64_t)((r[0] + (1u << k) - 1) >> k) * ((r[1] + (1u << k) - 1) >> k) *
                            ((r[2] + (1u << k) - 1) >> k);
@@ -2434,6 +2440,11 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         hipError_t le = hipGetLastError();
         if (sh == 2) {
             HIP_TRY(hipMemcpyAsync(c->d_occ, d_blob, nbw * 4, hipMemcpyDeviceToDevice, c->stream));
+        } else if (sh < 2) {                   // (ZRT_OCC_SH0 builds) bricks finer than OccX's
+            HIP_TRY(hipMemsetAsync(c->d_occ, 0, 4ull * c->occ_words, c->stream));
+            hipLaunchKernelGGL(occ_cells_kernel, dim3(4096), dim3(kBlock), 0, c->stream, c->d_cells, r[0], r[1],
+                               c->ncells, sh, c->occ_nb[0], c->occ_nb[0] * c->occ_nb[1], c->d_occ);
+            if (le == hipSuccess) le = hipGetLastError();
         } else {
             HIP_TRY(hipMemsetAsync(c->d_occ, 0, 4ull * c->occ_words, c->stream));
             hipLaunchKernelGGL(occ_coarsen_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0,
