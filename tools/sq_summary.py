@@ -22,7 +22,7 @@ import json
 import os
 import re
 
-KERNELS = (("wf_kernel<7, true>", r"wf_kernel<7, true"), ("wf_park_kernel", r"wf_park_kernel"),
+KERNELS = (("wf_kernel<6, true>", r"wf_kernel<\d, true"), ("wf_park_kernel", r"wf_park_kernel"),
            ("wf_shade_kernel", r"wf_shade_kernel"))
 
 

@@ -1694,8 +1694,11 @@ using WfFn = void (*)(const WfParams);
 #ifndef ZRT_WF_MINW
 #define ZRT_WF_MINW 6
 #endif
+// r04pw (the frustum-bound primary): 6 / 7 / 8 waves cfg3 5732 / 5724 / 5692,
+// cfg5 3491 / 3489 / 3493, cfg2 3778 / 3739 / 3725 Mrays/s; at 6 the primary
+// has no scratch access at all (12 at 7, 26 and walk reloads at 8)
 #ifndef ZRT_WF_MINW0
-#define ZRT_WF_MINW0 7
+#define ZRT_WF_MINW0 6
 #endif
 constexpr int kWfMinWaves = ZRT_WF_MINW;
 constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
