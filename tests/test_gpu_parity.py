@@ -244,9 +244,10 @@ def test_render_bitexact_vs_oracle(oracle_mod, gpu_scenes, name, camname, w, h, 
 # the default (wf_kernel primary launch, park + shade kernels for the
 # bounces) and per-lane walks everywhere (the fallback when OccX does not fit).
 # The park walk with and without the escape table (escape.h) on every scene,
-# whatever the density rule picks by default.
+# whatever the density rule picks by default; the primary with the frustum
+# bounds (escape.h frustum_bound), which small frames skip by default.
 MODES = [("default", 0), ("lane-walk", native.FLAG_LANE_WALK), ("escape", native.FLAG_ESCAPE),
-         ("no-escape", native.FLAG_NO_ESCAPE)]
+         ("no-escape", native.FLAG_NO_ESCAPE), ("frustum", native.FLAG_FRUSTUM)]
 
 
 @pytest.mark.parametrize("mode,flags", MODES, ids=[m for m, _ in MODES])
@@ -353,7 +354,7 @@ def test_frustum_bounds_random_cameras_identical(gpu_scenes, name):
         tgt = lo + ext * rng.random(3)
         cam = _look_camera(org, tgt, rng.uniform(0.2, 1.6), 36 + 4 * k, 29 + 3 * k)
         ref, r0 = rs.render(cam, num_samples=3, max_bounce=2, stats=True, linear=True)
-        img, r1 = rs.render(cam, num_samples=3, max_bounce=2, linear=True)
+        img, r1 = rs.render(cam, num_samples=3, max_bounce=2, linear=True, flags=native.FLAG_FRUSTUM)
         assert np.array_equal(ref, img), (k, inside)
         assert np.array_equal(r0["linear"], r1["linear"]), k
         assert r0["stats"]["segments"] == r1["stats"]["segments"], k

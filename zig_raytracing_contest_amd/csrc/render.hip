@@ -1760,6 +1760,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kPassSets = 2;
 constexpr uint32_t kMaxPassSets = 4;
 constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that runs kPassSets
+constexpr uint64_t kFrustumMinSamples = 1ull << 25; // samples of a frame that computes the frustum bounds
 // % of a pass moved from the last pass to the first when two sets run (r02d7,
 // vs 0: 20% cfg3 +3.2%, cfg5 +0.2%, cfg2 -1.0%; 16% cfg3 +1.4%; 25% cfg3
 // +3.2%, cfg2 -1.7%; the response is bumpy: r02d5/d6 sweeps)
@@ -1799,6 +1800,7 @@ struct zrt_context {
     // the primary frustum bounds (frustum_kernel) per 8x8 pixel block
     float4* d_tlo = nullptr; size_t tlo_cap = 0;
     bool esc_on = false;            // the park launches use it (dense enough to pay, context_escape)
+    bool esc_tried = false;         // context_escape ran (at the first render that can use it)
     double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
@@ -2465,8 +2467,9 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         c->occx_nbw = (uint32_t)nbw;
         c->occx_moff = (uint32_t)moff;
     }
-    int rc = context_sat(c);
-    if (rc == ZRT_OK) rc = context_escape(c);
+    // (the escape table itself is built by the first render whose frame is
+    // large enough to pay for it: context_escape)
+    const int rc = context_sat(c);
     if (rc != ZRT_OK) return rc;
     return context_counters(c);
 }
@@ -2780,6 +2783,13 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
     // the escape table: where dense enough to pay (context_escape), or as
     // the flags force it (both kernels give the same image)
+    // (built at the first frame of 2^23 samples or more, or the first the flag
+    // forces: 2.1 ms on cfg3 at 384 bins, r04eb2, more than the table saves a
+    // 3-spp 1080p frame)
+    if (!c->esc_tried && park_next && !(cfg->flags & ZRT_FLAG_NO_ESCAPE) && (big || (cfg->flags & ZRT_FLAG_ESCAPE))) {
+        c->esc_tried = true;
+        if ((rc = context_escape(c)) != ZRT_OK) return rc;
+    }
     const bool esc = c->d_esc && !(cfg->flags & ZRT_FLAG_NO_ESCAPE) &&
                      (c->esc_on || (cfg->flags & ZRT_FLAG_ESCAPE));
     const WfFn f_next = park_next ? (esc ? (WfFn)wf_park_kernel<true> : (WfFn)wf_park_kernel<false>)
@@ -2922,7 +2932,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 512, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
-    if (ZRT_FRUSTUM && c->d_sat && !counting && packed) {
+    // the frustum bounds cost a 0.42-ms launch per render (cfg3, r04eb2) and
+    // save ~18% of the primary launch: frames of 2^25 samples or more
+    if (ZRT_FRUSTUM && c->d_sat && !counting && packed &&
+        ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
         // timed region: 32 K threads for a 1080p frame)
         const uint32_t nbx = (cam->w + 7u) / 8u, nby = (cam->h + 7u) / 8u;
