@@ -1760,7 +1760,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kPassSets = 2;
 constexpr uint32_t kMaxPassSets = 4;
 constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that runs kPassSets
-constexpr uint64_t kFrustumMinSamples = 1ull << 25; // samples of a frame that computes the frustum bounds
+constexpr uint64_t kFrustumMinSamples = 1ull << 24; // samples of a frame that computes the frustum bounds
 // % of a pass moved from the last pass to the first when two sets run (r02d7,
 // vs 0: 20% cfg3 +3.2%, cfg5 +0.2%, cfg2 -1.0%; 16% cfg3 +1.4%; 25% cfg3
 // +3.2%, cfg2 -1.7%; the response is bumpy: r02d5/d6 sweeps)
@@ -2933,7 +2933,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 512, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
     // the frustum bounds cost a 0.42-ms launch per render (cfg3, r04eb2) and
-    // save ~18% of the primary launch: frames of 2^25 samples or more
+    // save ~18% of the primary launch: frames of 2^24 samples or more (cfg2's
+    // 512^2 x 64 gains 1.9% with them, r04s; a 3-spp 1080p frame's primary
+    // takes ~0.5 ms)
     if (ZRT_FRUSTUM && c->d_sat && !counting && packed &&
         ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
