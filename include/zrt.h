@@ -129,7 +129,7 @@ typedef struct zrt_render_config {
                                         scenes where enough of it is set to pay); same image */
 #define ZRT_FLAG_NO_ESCAPE    0x80u  /* the park walk never uses the escape table; same image */
 #define ZRT_FLAG_FRUSTUM      0x100u /* the primary launch always uses the frustum bounds (by default
-                                        only for frames of 2^24 samples or more, where their build pays);
+                                        only for frames of 2^23 samples or more, where their build pays);
                                         same image */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +

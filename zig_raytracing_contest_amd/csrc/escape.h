@@ -143,22 +143,34 @@ constexpr int kFrustumGapSlices = 2;
 struct FrustumBound {
     float lo, hi, ga, gb;
 };
-ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const float bmin[3], const float bmax[3],
-                               const float cs[3], const float org[3], const float llc[3], const float right[3],
-                               const float up[3], double u0, double u1, double v0, double v1) {
-    FrustumBound fb{0.0f, kInf, kInf, kInf};
+ZHD bool s_far_finite(double x) { return x * 0.0 == 0.0; }
+
+// The block's cone: corner directions, |D| bounds, the march's slice width
+// along the dominant axis and its end (frustum_bound; frustum_kernel runs the
+// slices over a wave's lanes with the same arithmetic).
+struct FrustumCone {
     double D[4][3];
+    double dmin, dmax, s_far, ds;
+    bool ok;
+};
+ZHD FrustumCone frustum_cone(const float bmin[3], const float bmax[3], const float cs[3], const float org[3],
+                             const float llc[3], const float right[3], const float up[3], double u0, double u1,
+                             double v0, double v1) {
+    FrustumCone q;
+    q.ok = false;
+    q.dmax = 0.0;
+    q.s_far = q.ds = 0.0;
     const double uu[2] = {u0, u1}, vv[2] = {v0, v1};
-    double dmin = 1e300, dmax = 0.0, mid[3] = {0, 0, 0};
+    double dmin = 1e300, mid[3] = {0, 0, 0};
     for (int c = 0; c < 4; ++c) {
         double n2 = 0.0;
         for (int k = 0; k < 3; ++k) {
-            D[c][k] = (double)llc[k] + (double)right[k] * uu[c & 1] + (double)up[k] * vv[c >> 1];
-            n2 += D[c][k] * D[c][k];
-            mid[k] += 0.25 * D[c][k];
+            q.D[c][k] = (double)llc[k] + (double)right[k] * uu[c & 1] + (double)up[k] * vv[c >> 1];
+            n2 += q.D[c][k] * q.D[c][k];
+            mid[k] += 0.25 * q.D[c][k];
         }
         dmin = fmin(dmin, sqrt(n2));
-        dmax = fmax(dmax, sqrt(n2));
+        q.dmax = fmax(q.dmax, sqrt(n2));
     }
     // |D| over the parallelogram >= the corners' least |D| minus its diagonals
     double rl = 0.0, ul = 0.0;
@@ -167,65 +179,83 @@ ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const flo
         ul += (double)up[k] * up[k];
     }
     dmin -= sqrt(rl) * (u1 - u0) + sqrt(ul) * (v1 - v0);
-    if (!(dmin > 0.0)) return fb;
+    q.dmin = dmin;
+    if (!(dmin > 0.0)) return q;
     // beyond s_far every point of the cone is farther from o than any grid point
     double far2 = 0.0;
     for (int k = 0; k < 3; ++k) {
         const double a = fabs((double)bmin[k] - org[k]), b = fabs((double)bmax[k] - org[k]);
         far2 += fmax(a, b) * fmax(a, b);
     }
-    const double s_far = sqrt(far2) / dmin;
+    q.s_far = sqrt(far2) / dmin;
     int ax = 0;
     for (int k = 1; k < 3; ++k)
         if (fabs(mid[k]) / cs[k] > fabs(mid[ax]) / cs[ax]) ax = k;
-    const double ds = 2.0 * (double)cs[ax] / fmax(fabs(mid[ax]), 1e-30);
-    if (!(ds > 0.0)) return fb;
-    double first = -1.0, last = -1.0, gap_s = -1.0, best0 = 0.0, best1 = 0.0, best_len = -1.0;
-    int run = 0;
-    for (int it = 0; it < 1 << 16; ++it) {
-        const double s0 = it * ds, s1 = s0 + ds;
-        if (s0 > s_far) break;
-        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-        for (int c = 0; c < 4; ++c)
-            for (int k = 0; k < 3; ++k) {
-                const double p0 = org[k] + s0 * D[c][k], p1 = org[k] + s1 * D[c][k];
-                lo[k] = fmin(lo[k], fmin(p0, p1));
-                hi[k] = fmax(hi[k], fmax(p0, p1));
-            }
-        uint32_t c0[3], c1[3];
-        bool outside = false;
+    q.ds = 2.0 * (double)cs[ax] / fmax(fabs(mid[ax]), 1e-30);
+    // the march must reach s_far within its 2^16 slices
+    q.ok = q.ds > 0.0 && s_far_finite(q.s_far) && (double)(1 << 16) * q.ds > q.s_far;
+    return q;
+}
+// Slice it of the march: [it ds, it ds + ds]; whether its box (the eight
+// corner points, dilated by one cell) holds an occupied cell.
+ZHD bool frustum_slice(const EscSat& S, const FrustumCone& q, const uint32_t res[3], const float bmin[3],
+                       const float cs[3], const float org[3], int it) {
+    const double s0 = it * q.ds, s1 = s0 + q.ds;
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int c = 0; c < 4; ++c)
         for (int k = 0; k < 3; ++k) {
-            const double a = floor((lo[k] - bmin[k]) / cs[k]) - 1.0, b = floor((hi[k] - bmin[k]) / cs[k]) + 1.0;
-            if (b < 0.0 || a > res[k] - 1.0) { outside = true; break; }
-            c0[k] = (uint32_t)fmax(0.0, a);
-            c1[k] = (uint32_t)fmin(res[k] - 1.0, b);
+            const double p0 = org[k] + s0 * q.D[c][k], p1 = org[k] + s1 * q.D[c][k];
+            lo[k] = fmin(lo[k], fmin(p0, p1));
+            hi[k] = fmax(hi[k], fmax(p0, p1));
         }
-        if (!outside && esc_box(S, c0[0], c1[0], c0[1], c1[1], c0[2], c1[2]) != 0u) {
-            if (first >= 0.0 && run >= kFrustumGapSlices && (s0 * dmin - gap_s * dmax) > best_len) {
-                best_len = s0 * dmin - gap_s * dmax;
-                best0 = gap_s;
-                best1 = s0;
-            }
-            if (first < 0.0) first = s0;
-            last = s1;
-            run = 0;
-        } else {
-            if (run == 0) gap_s = s0;
-            ++run;
-        }
+    uint32_t c0[3], c1[3];
+    for (int k = 0; k < 3; ++k) {
+        const double a = floor((lo[k] - bmin[k]) / cs[k]) - 1.0, b = floor((hi[k] - bmin[k]) / cs[k]) + 1.0;
+        if (b < 0.0 || a > res[k] - 1.0) return false;
+        c0[k] = (uint32_t)fmax(0.0, a);
+        c1[k] = (uint32_t)fmin(res[k] - 1.0, b);
     }
-    if (!(s_far * 0.0 == 0.0) || (double)(1 << 16) * ds <= s_far) return fb;   // the march did not reach s_far
-    if (first < 0.0) {
+    return esc_box(S, c0[0], c1[0], c0[1], c1[1], c0[2], c1[2]) != 0u;
+}
+// lo and hi from the first and last occupied slices (-1: none).
+ZHD void frustum_finish(const FrustumCone& q, int first, int last, FrustumBound& fb) {
+    if (first < 0) {
         fb.lo = kInf;
-        return fb;
+        return;
     }
-    const double tl = first * dmin, th = last * dmax;
+    const double tl = (first * q.ds) * q.dmin, th = (last * q.ds + q.ds) * q.dmax;
     fb.lo = (float)tl;
     if ((double)fb.lo > tl) fb.lo = nextafterf(fb.lo, 0.0f);     // round down
     fb.hi = (float)th;
     if ((double)fb.hi < th) fb.hi = nextafterf(fb.hi, kInf);     // round up
-    if (best_len > 0.0) {
-        const double ta = best0 * dmax, tb = best1 * dmin;
+}
+ZHD FrustumBound frustum_bound(const EscSat& S, const uint32_t res[3], const float bmin[3], const float bmax[3],
+                               const float cs[3], const float org[3], const float llc[3], const float right[3],
+                               const float up[3], double u0, double u1, double v0, double v1) {
+    FrustumBound fb{0.0f, kInf, kInf, kInf};
+    const FrustumCone q = frustum_cone(bmin, bmax, cs, org, llc, right, up, u0, u1, v0, v1);
+    if (!q.ok) return fb;                                          // no bound
+    int first = -1, last = -1, gap_it = -1, best0 = 0, best1 = 0, run = 0;
+    double best_len = -1.0;
+    for (int it = 0; it < 1 << 16 && !(it * q.ds > q.s_far); ++it) {
+        if (frustum_slice(S, q, res, bmin, cs, org, it)) {
+            const double len = (it * q.ds) * q.dmin - (gap_it * q.ds) * q.dmax;
+            if (first >= 0 && run >= kFrustumGapSlices && len > best_len) {
+                best_len = len;
+                best0 = gap_it;
+                best1 = it;
+            }
+            if (first < 0) first = it;
+            last = it;
+            run = 0;
+        } else {
+            if (run == 0) gap_it = it;
+            ++run;
+        }
+    }
+    frustum_finish(q, first, last, fb);
+    if (first >= 0 && best_len > 0.0) {
+        const double ta = (best0 * q.ds) * q.dmax, tb = (best1 * q.ds) * q.dmin;
         float ga = (float)ta, gb = (float)tb;
         if ((double)ga < ta) ga = nextafterf(ga, kInf);          // round up
         if ((double)gb > tb) gb = nextafterf(gb, 0.0f);          // round down

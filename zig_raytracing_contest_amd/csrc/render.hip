@@ -1760,7 +1760,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kPassSets = 2;
 constexpr uint32_t kMaxPassSets = 4;
 constexpr uint64_t kSetsMinSamples = 1ull << 23;   // samples of a frame that runs kPassSets
-constexpr uint64_t kFrustumMinSamples = 1ull << 24; // samples of a frame that computes the frustum bounds
+constexpr uint64_t kFrustumMinSamples = 1ull << 23; // samples of a frame that computes the frustum bounds
 // % of a pass moved from the last pass to the first when two sets run (r02d7,
 // vs 0: 20% cfg3 +3.2%, cfg5 +0.2%, cfg2 -1.0%; 16% cfg3 +1.4%; 25% cfg3
 // +3.2%, cfg2 -1.7%; the response is bumpy: r02d5/d6 sweeps)
@@ -2288,13 +2288,44 @@ struct FrustumArgs {
 };
 __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
                                                          float4* __restrict__ tlo) {
+    const EscSat S{sat, a.res[0] + 1u, (a.res[0] + 1u) * (a.res[1] + 1u)};
+#if ZRT_FRUSTUM_GAP
+    // one thread per block: frustum_bound's serial march (the gap needs it)
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= a.nbx * a.nby) return;
     const uint32_t bx = b % a.nbx, by = b / a.nbx;
-    const EscSat S{sat, a.res[0] + 1u, (a.res[0] + 1u) * (a.res[1] + 1u)};
     const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx,
                                           8.0 * bx + 8.0, 8.0 * by, 8.0 * by + 8.0);
     tlo[b] = make_float4(fb.lo, fb.hi, fb.ga, fb.gb);
+#else
+    // one wave per block: lane l tests slices l, l + 64, ... of the same
+    // march (frustum_cone / frustum_slice), the wave takes the first and
+    // last occupied ones (a 1080p frame: 32 K waves of ~4 slices per lane
+    // instead of 32 K threads of ~200 dependent slices, 0.42 ms, r04eb2)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t b = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    if (b >= a.nbx * a.nby) return;                        // (uniform over the wave)
+    const uint32_t bx = b % a.nbx, by = b / a.nbx;
+    const FrustumCone q = frustum_cone(a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx, 8.0 * bx + 8.0,
+                                       8.0 * by, 8.0 * by + 8.0);
+    int first = 1 << 30, last = -1;
+    if (q.ok)
+        for (int it = (int)lane; it < (1 << 16) && !(it * q.ds > q.s_far); it += 64)
+            if (frustum_slice(S, q, a.res, a.bmin, a.cs, a.org, it)) {
+                first = min(first, it);
+                last = max(last, it);
+            }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        first = min(first, __shfl_xor(first, off));
+        last = max(last, __shfl_xor(last, off));
+    }
+    if (lane == 0) {
+        FrustumBound fb{0.0f, kInf, kInf, kInf};
+        if (q.ok) frustum_finish(q, first == (1 << 30) ? -1 : first, last, fb);
+        tlo[b] = make_float4(fb.lo, fb.hi, kInf, kInf);
+    }
+#endif
 }
 
 // The summed-area table of cell occupancy (escape.h EscSat): kept in the
@@ -2932,10 +2963,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 512, c->stream));
     HIP_TRY(hipEventRecord(c->ev_begin, c->stream));
-    // the frustum bounds cost a 0.42-ms launch per render (cfg3, r04eb2) and
-    // save ~18% of the primary launch: frames of 2^24 samples or more (cfg2's
-    // 512^2 x 64 gains 1.9% with them, r04s; a 3-spp 1080p frame's primary
-    // takes ~0.5 ms)
+    // the frustum bounds cost a 78-us launch per render (1080p, one wave per
+    // block, r04fk3; 0.42 ms one thread per block) and save ~18% of the
+    // primary launch: frames of 2^23 samples or more (a 3-spp 1080p frame's
+    // primary takes ~0.5 ms: break-even)
     if (ZRT_FRUSTUM && c->d_sat && !counting && packed &&
         ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
@@ -2954,7 +2985,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             fa.up[k] = cam->up[k];
         }
         fa.w = cam->w; fa.h = cam->h; fa.nbx = nbx; fa.nby = nby;
-        hipLaunchKernelGGL(frustum_kernel, dim3((nbx * nby + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+        const uint64_t fthreads = (uint64_t)nbx * nby * (ZRT_FRUSTUM_GAP ? 1u : 64u);
+        hipLaunchKernelGGL(frustum_kernel, dim3((uint32_t)((fthreads + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                            (const uint32_t*)c->d_sat, fa, c->d_tlo);
         HIP_TRY(hipGetLastError());
         tp.tlo = c->d_tlo;
