@@ -31,8 +31,9 @@ Beside the timed loop (rank 0, N = 1, after it):
          fewer GPUs than asked (the reference's partition, stage3.zig:228-229).
 
 Rank 0 prints ONE JSON line, with the sha1 of the whole frame (img_sha1: the
-same for any N, asserted equal to the untimed counting frame's).  Image tiles
-(64x64, interleaved t % N) shard the frame: total work is fixed as N grows
+same for any N, asserted equal to the untimed counting frame's and to the CPU
+oracle's whole-frame hash in tests/golden/frames.json: oracle_frame_match).
+Image tiles (32x32 over several ranks, interleaved t % N) shard the frame: total work is fixed as N grows
 ("scaling": "strong").  The roofline block is the dominant kernel's, from one
 extra frame on one HIP stream (exclusive kernel durations).
 """
@@ -260,6 +261,17 @@ def wall_clock(soup, cfgd, reps=3, cpu=True):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def frame_golden(config):
+    """The CPU oracle's whole-frame hashes of a BASELINE config
+    (tests/golden/frames.json, written by tools/make_frame_golden.py in the
+    build container); None when the config has none."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "frames.json")) as fh:
+            return json.load(fh).get(config)
+    except (OSError, ValueError):
+        return None
+
+
 def roofline_profile_for(config, one_set_kernel="wf_park_kernel"):
     """The newest committed per-kernel counter profile of this workload
     (tools/roofline_profile.py over rocprofv3 passes of `bench.py --one-set`:
@@ -432,6 +444,16 @@ def main():
         assert cst["segments"] * a.steps == segs, "counting and timed kernels disagree"
         img_sha1 = frame_sha1(img)
         assert img_sha1 == count_sha1, "the timed frame differs from the counting frame"
+        # the whole frame against the CPU oracle's (tools/make_frame_golden.py:
+        # every pixel of the frame through oracle/zrt_oracle.c, the
+        # reference's renderWorker restated, in the counter-RNG mode)
+        golden = frame_golden(a.config) if spp == cfgd["spp"] else None
+        oracle_match = None
+        if golden is not None:
+            oracle_match = (img_sha1 == golden["rgb8_sha1"] and
+                            int(total_segs / a.steps) == golden["segments"])
+            assert oracle_match, (f"frame differs from the oracle's: sha1 {img_sha1} vs {golden['rgb8_sha1']}, "
+                                  f"segments {int(total_segs / a.steps)} vs {golden['segments']}")
         # ---- roofline of the dominant kernel.  The timed frames run two
         # pass sets on two HIP streams, so their kernels overlap and no
         # kernel's duration is its own.  One more frame (after the timed
@@ -496,14 +518,20 @@ def main():
             "GB_per_launch": round(alg_per_launch / 1e9, 3),
             "achieved": round(alg_per_launch / launch_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(alg_per_launch / launch_s / 1e9 / PEAK_HBM_GBS, 4)}
-        # the whole frame's d4 rate over the timed (two-stream) frames: round
-        # 2's figure, kept for continuity
+        # the whole frame's d4 bytes over the timed (two-stream) frames: the
+        # reference's memory work per second (every cell it visits, every
+        # triangle it tests).  A work rate, not a fraction of HBM: the GPU
+        # answers most of those cells from LDS and the escape / frustum tables
+        # without reading them, so no peak fraction is given.
         frame_alg = (B_CELL * cst["cells_visited"] + B_TRI * cst["triangle_tests"] + B_HIT * cst["hits"] + B_PIX * P)
-        roof["frame_algorithmic"] = {"GB_per_frame": round(frame_alg / 1e9, 1),
-                                     "GBps": round(frame_alg * a.steps / (gpu_ms / 1e3) / 1e9, 1),
-                                     "frac": round(frame_alg * a.steps / (gpu_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
-                                     "gpu_ms_per_step": round(gpu_ms / a.steps, 3),
-                                     "avg_launch_ms_overlapped": round(kern_ms / max(launches, 1), 3)}
+        roof["reference_equivalent_rate"] = {
+            "what": "SURVEY.md d4 bytes of the reference's whole-frame work (8 B per cell visited, 36 B per "
+                    "triangle test, hit data + texels, 3 B per pixel) per second of the timed frames; "
+                    "NOT DRAM traffic and not comparable with the HBM peak",
+            "GB_per_frame": round(frame_alg / 1e9, 1),
+            "GBps": round(frame_alg * a.steps / (gpu_ms / 1e3) / 1e9, 1),
+            "gpu_ms_per_step": round(gpu_ms / a.steps, 3),
+            "avg_launch_ms_overlapped": round(kern_ms / max(launches, 1), 3)}
         out = {
             "metric": "Mrays/sec + wall-clock to output.png on contest config.json scene",
             "value": round(total_segs / elapsed / 1e6, 3),
@@ -521,6 +549,11 @@ def main():
                        "schedule": "one pass set (profiling)" if a.one_set else
                                    f"{cprof['passes']} counting passes; timed: default pass sets"},
             "img_sha1": img_sha1,
+            "oracle_frame_match": oracle_match,
+            "oracle_frame": None if golden is None else {
+                "rgb8_sha1": golden["rgb8_sha1"], "segments": golden["segments"],
+                "source": "tests/golden/frames.json (tools/make_frame_golden.py: the CPU oracle over every "
+                          "pixel, RNG_PATH mode)"},
             "roofline": roof,
             "work": {k: int(cst[k]) for k in ("segments", "cells_visited", "triangle_tests",
                                                "hits", "samples")},

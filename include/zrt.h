@@ -108,7 +108,8 @@ typedef struct zrt_render_config {
                                         passes as 144 GiB of path queues allow, at least two for frames
                                         of 2^23 samples or more (the image is the same for any value) */
     /* zrt_render only (ABI 2, in what were reserved words; zero = `device`
-     * alone): the image's tiles split over num_devices HIP ordinals, tile t
+     * alone, one = devices[0] alone): the image's tiles split over
+     * num_devices HIP ordinals, tile t
      * rendered on devices[t % num_devices] (repeats allowed), gathered into
      * rgb_out over xGMI -- the multi-device fan-out and join that
      * Scene.render does with its worker threads (stage3.zig:247-256). */
@@ -183,8 +184,9 @@ void zrt_geometry_free(zrt_geometry* g);
 
 /* One-shot drop-in for Scene.render: uploads the scene, renders the whole
  * image on `cfg->device` -- or, with cfg->num_devices > 1, on every device of
- * cfg->devices (one host thread and one context per entry, interleaved 64x64
- * tiles, the packed tiles gathered to the first device over xGMI) -- writes
+ * cfg->devices (one host thread and one context per entry, interleaved 32x32
+ * tiles by default -- cfg->tile_size overrides -- the packed tiles gathered
+ * to the first device over xGMI) -- writes
  * w*h*3 RGB8 into rgb_out (caller-allocated, row 0 = top), frees device
  * memory, returns.  The image is bit-identical for any device list. */
 int zrt_render(const zrt_scene* scene, const zrt_camera* camera, const zrt_render_config* cfg,

@@ -239,6 +239,27 @@ int main(int argc, char** argv) {
            (unsigned long long)f_far, (unsigned long long)f_far_unsound, (unsigned long long)f_gap_blocks,
            (unsigned long long)f_gap, (unsigned long long)f_gap_unsound);
     unsound += f_unsound + f_far_unsound + f_gap_unsound;
+    // flat grids (a zero or non-finite cell_size axis, linalg.zig:412-441 on
+    // coplanar scenes): no escape bit and no frustum bound, whatever the
+    // occupancy (the kernels' guard against dividing by them)
+    uint64_t flat_bits = 0, flat_bounds = 0;
+    {
+        const uint32_t fres[3] = {8, 8, 8};
+        std::vector<uint32_t> fsat(9 * 9 * 9, 0u);    // an empty grid: every bit would be set
+        const EscSat FS{fsat.data(), 9u, 81u};
+        const float bad[4][3] = {{0.5f, 0.5f, 0.0f}, {0.0f, 0.5f, 0.5f}, {0.0f, 0.0f, 0.0f},
+                                 {0.5f, kInf, 0.5f}};
+        for (const auto& c3 : bad) {
+            for (uint32_t bin = 0; bin < kEscNBin; ++bin) flat_bits += esc_compute(FS, fres, c3, 0, 1, 0, bin);
+            const float fbmin[3] = {0, 0, 0}, fbmax[3] = {4 * c3[0], 4 * c3[1], 4 * c3[2]};
+            const float forg[3] = {-1, -2, -3}, fllc[3] = {1, 2, 3}, fr[3] = {0.01f, 0, 0}, fu[3] = {0, 0.01f, 0};
+            const FrustumBound fb = frustum_bound(FS, fres, fbmin, fbmax, c3, forg, fllc, fr, fu, 0, 8, 0, 8);
+            flat_bounds += !(fb.lo == 0.0f && fb.hi == kInf);
+        }
+    }
+    printf("{\"flat_grid_bits\": %llu, \"flat_grid_bounds\": %llu}\n", (unsigned long long)flat_bits,
+           (unsigned long long)flat_bounds);
+    unsound += flat_bits + flat_bounds;
     printf("{\"rays\": %llu, \"steps\": %llu, \"escapes\": %llu, \"steps_after_escape\": %llu, \"bits_set\": %.4f, "
            "\"unsound\": %llu, \"box_fails\": %llu}\n",
            (unsigned long long)rays, (unsigned long long)steps, (unsigned long long)escapes,

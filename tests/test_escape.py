@@ -42,3 +42,5 @@ def test_escape_table_is_sound(tmp_path):
     # the gap: no occupied cell entered inside it, and it holds cells
     assert res["frustum_gap_unsound"] == 0, res
     assert res["frustum_gap_blocks"] > 20 and res["frustum_cells_in_gap"] > 5000, res
+    # zero / non-finite cell_size axes: no proof at all
+    assert res["flat_grid_bits"] == 0 and res["flat_grid_bounds"] == 0, res

@@ -13,7 +13,15 @@ oracle side costs seconds.
 
 A frame's pixels are independent (the RNG is keyed by pixel and sample), so
 a pixel's value does not depend on which other pixels the oracle renders.
+
+Whole frames: tools/make_frame_golden.py ran the oracle over
+EVERY pixel of cfg2/cfg3/cfg5/cfg4 in the build container and committed the
+RGB8 and linear-radiance sha1 of each frame and its segment count
+(tests/golden/frames.json); the same renders are hashed whole against them,
+and cfg2 is also compared pixel for pixel with a live whole-frame oracle run.
 """
+import hashlib
+import json
 import os
 
 import numpy as np
@@ -36,6 +44,28 @@ def _subset(w, h, stride=499, tile=64):
         for y in range(ty, min(h, ty + tile)):
             pix.update(range(y * w + tx, y * w + min(w, tx + tile)))
     return np.array(sorted(pix), np.uint32)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+with open(os.path.join(ROOT, "tests", "golden", "frames.json")) as _fh:
+    GOLDEN = json.load(_fh)
+
+
+def _row_major(packed_vals, w, h, tile=0):
+    """A packed-order (zrt_tile_pixels) per-pixel array back in row-major order."""
+    pix = native.tile_pixels(w, h) if tile == 0 else native.tile_pixels(w, h, tile)
+    full = np.zeros((w * h,) + packed_vals.shape[1:], packed_vals.dtype)
+    full[pix] = packed_vals
+    return full
+
+
+def _check_whole_frame(cfg, rgb_row_major, lin_row_major, segments):
+    g = GOLDEN[cfg]
+    assert segments == g["segments"], (segments, g["segments"])
+    assert hashlib.sha1(np.ascontiguousarray(rgb_row_major, np.uint8).tobytes()).hexdigest() == g["rgb8_sha1"]
+    if lin_row_major is not None:
+        assert hashlib.sha1(np.ascontiguousarray(lin_row_major, np.float32).tobytes()).hexdigest() == \
+            g["linear_sha1"]
 
 
 # (config, passes the default split must produce at that size: the schedule
@@ -70,3 +100,50 @@ def test_benchmark_frame_subset_bitexact(oracle_mod, cfg, min_passes):
     bad = np.flatnonzero(np.any(gpu_rgb != rgb, axis=1))
     assert bad.size == 0, f"{bad.size} of {pixels.size} pixels differ, first {pixels[bad[:5]]}"
     assert np.array_equal(gpu_lin.view(np.uint32), lin.view(np.uint32))
+    # and the whole frame against the oracle's whole-frame hashes
+    _check_whole_frame(cfg, img.reshape(-1, 3), _row_major(res["linear"], cam.w, cam.h),
+                       res["stats"]["segments"])
+
+
+def test_cfg2_whole_frame_vs_live_oracle(oracle_mod):
+    """cfg2 (Cornell 512^2, 64 spp) in full on both sides: every pixel's RGB8
+    and linear radiance bit-equal, and the traversal counters equal (the
+    oracle takes ~10-20 s on the host's cores)."""
+    d = scenes.CONFIGS["cfg2"]
+    soup = scenes.get_scene(d["scene"])
+    c = soup.camera(d["camera"])
+    cam = camera_for(soup, d["camera"], d["width"], d["height"])
+    rs = RenderScene(soup, device=0)
+    try:
+        img, res = rs.render(cam, num_samples=d["spp"], max_bounce=d["max_bounce"], linear=True)
+        _, cres = rs.render(cam, num_samples=d["spp"], max_bounce=d["max_bounce"], stats=True)
+    finally:
+        rs.close()
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, c.aspect, d["width"], d["height"])
+    rgb, lin, ctr = oracle_mod.OracleScene(soup).render(ocam, d["spp"], d["max_bounce"], oracle_mod.RNG_PATH, 0,
+                                                        _threads())
+    assert np.array_equal(img.reshape(-1, 3), rgb)
+    assert np.array_equal(_row_major(res["linear"], cam.w, cam.h).view(np.uint32), lin.view(np.uint32))
+    st = cres["stats"]
+    assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == tuple(int(x) for x in ctr[:4])
+    _check_whole_frame("cfg2", rgb, lin, int(ctr[0]))
+
+
+def test_cfg4_on_a_repeated_device_group_whole_frame():
+    """cfg4 (4K, 1024 spp: ~1 TB of path queues, many passes) split over a
+    group that lists GPU 0 twice: the two contexts render side by side and
+    each sizes its passes from half the device's queue budget (each
+    used to claim 60% of the same free HBM); the gathered frame equals the
+    oracle's whole-frame hash."""
+    d = scenes.CONFIGS["cfg4"]
+    soup = scenes.get_scene(d["scene"])
+    cam = camera_for(soup, d["camera"], d["width"], d["height"])
+    geo = native.Geometry(soup.pos, soup.nrm, soup.uv, soup.mat)
+    keep = []
+    native.attach_materials(geo.scene, soup.tex_desc, soup.texels, keep)
+    grp = native.Group(geo.scene, [0, 0])
+    try:
+        img, st = grp.render(cam, d["spp"], d["max_bounce"])
+    finally:
+        grp.close()
+    _check_whole_frame("cfg4", img.reshape(-1, 3), None, st["segments"])

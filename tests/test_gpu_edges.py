@@ -104,29 +104,45 @@ def soups():
     return get
 
 
+_ORACLE = {}
+
+# the timed kernels' variants: defaults, the escape table
+# forced on / off (wf_park_kernel<true> / <false>) and the primary frustum
+# bounds forced on (small frames skip them by default): every one of them on
+# every degenerate grid (flat, 1x1x1, 3x5x2, coarse bricks, wide axes, sky)
+MODES = {"default": 0, "escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
+         "frustum": native.FLAG_FRUSTUM}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("device_build", [False, True], ids=["host-build", "device-build"])
 @pytest.mark.parametrize("name,w,h,spp,mb,res", CASES)
-def test_edge_render_bitexact_vs_oracle(oracle_mod, soups, name, w, h, spp, mb, res, device_build):
+def test_edge_render_bitexact_vs_oracle(oracle_mod, soups, name, w, h, spp, mb, res, device_build, mode):
     soup = soups(name)
     cam = camera_for(soup, None, w, h)
+    key = (name, w, h, spp, mb, res)
+    if key not in _ORACLE:
+        c = soup.camera(None)
+        ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
+        _ORACLE[key] = oracle_mod.OracleScene(soup, res).render(ocam, spp, mb, oracle_mod.RNG_PATH, 0, 16)
+    rgb, lin, ctr = _ORACLE[key]
+    pix = native.tile_pixels(cam.w, cam.h)
     rs = RenderScene(soup, res, device_build=device_build)
     try:
-        img, out = rs.render(cam, num_samples=spp, max_bounce=mb, stats=True, linear=True)
-        fast, _ = rs.render(cam, num_samples=spp, max_bounce=mb)   # timed kernels
+        if mode == "default":   # the counting build (trace_kernel): the counters
+            img, out = rs.render(cam, num_samples=spp, max_bounce=mb, stats=True, linear=True)
+            assert np.array_equal(out["linear"].view(np.uint32), lin[pix].view(np.uint32))
+            assert np.array_equal(img.reshape(-1, 3), rgb)
+            st = out["stats"]
+            assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == \
+                tuple(int(x) for x in ctr[:4])
+            if name == "sky_only":   # the walk still runs: the box behind the camera is entered
+                assert st["hits"] == 0
+        fast, fo = rs.render(cam, num_samples=spp, max_bounce=mb, linear=True, flags=MODES[mode])
     finally:
         rs.close()
-    c = soup.camera(None)
-    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
-    rgb, lin, ctr = oracle_mod.OracleScene(soup, res).render(ocam, spp, mb, oracle_mod.RNG_PATH, 0, 16)
-    pix = native.tile_pixels(cam.w, cam.h)
-    assert np.array_equal(out["linear"].view(np.uint32), lin[pix].view(np.uint32))
-    assert np.array_equal(img.reshape(-1, 3), rgb)
-    assert np.array_equal(fast, img)
-    st = out["stats"]
-    assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == \
-        tuple(int(x) for x in ctr[:4])
-    if name == "sky_only":   # the walk still runs: the box behind the camera is entered
-        assert st["hits"] == 0
+    assert np.array_equal(fast.reshape(-1, 3), rgb)
+    assert np.array_equal(fo["linear"].view(np.uint32), lin[pix].view(np.uint32))
 
 
 def test_growing_frames_counting_timed_counting(oracle_mod):

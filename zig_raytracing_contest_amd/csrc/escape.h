@@ -74,8 +74,17 @@ ZHD uint32_t esc_box(const EscSat& S, uint32_t x0, uint32_t x1, uint32_t y0, uin
 }
 
 // The bit of brick (bx, by, bz) and `bin` (see the header comment).
+// A grid with a zero-extent (or non-finite) axis -- every triangle in one
+// plane, Grid.init's cell_size 0 (linalg.zig:412-441) -- has walks whose
+// crossings on that axis do not advance t, which the cell-unit geometry below
+// does not model: such grids get no proof (no escape bit, no frustum bound).
+ZHD bool esc_cells_regular(const float cs[3]) {
+    return cs[0] > 0.0f && cs[1] > 0.0f && cs[2] > 0.0f && cs[0] < kInf && cs[1] < kInf && cs[2] < kInf;
+}
+
 ZHD bool esc_compute(const EscSat& S, const uint32_t res[3], const float cs[3], uint32_t bx, uint32_t by,
                      uint32_t bz, uint32_t bin) {
+    if (!esc_cells_regular(cs)) return false;
     const uint32_t fc = bin / (kEscBins * kEscBins), iu = (bin / kEscBins) % kEscBins, iv = bin % kEscBins;
     const int a = (int)(fc / 2u), sg = (fc & 1u) ? -1 : 1;
     const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
@@ -180,7 +189,7 @@ ZHD FrustumCone frustum_cone(const float bmin[3], const float bmax[3], const flo
     }
     dmin -= sqrt(rl) * (u1 - u0) + sqrt(ul) * (v1 - v0);
     q.dmin = dmin;
-    if (!(dmin > 0.0)) return q;
+    if (!(dmin > 0.0) || !esc_cells_regular(cs)) return q;
     // beyond s_far every point of the cone is farther from o than any grid point
     double far2 = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -209,6 +218,7 @@ ZHD bool frustum_slice(const EscSat& S, const FrustumCone& q, const uint32_t res
             hi[k] = fmax(hi[k], fmax(p0, p1));
         }
     uint32_t c0[3], c1[3];
+    if (!esc_cells_regular(cs)) return true;                  // (no bound: frustum_cone refuses these)
     for (int k = 0; k < 3; ++k) {
         const double a = floor((lo[k] - bmin[k]) / cs[k]) - 1.0, b = floor((hi[k] - bmin[k]) / cs[k]) + 1.0;
         if (b < 0.0 || a > res[k] - 1.0) return false;

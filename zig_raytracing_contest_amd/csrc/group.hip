@@ -4,7 +4,7 @@
 // Reference: Scene.render (src/stage3.zig:247-256) spawns one worker per
 // thread over contiguous pixel blocks (stage3.zig:228-229) and joins them
 // before it returns.  Here the workers are GPUs: one context per device, the
-// image's 64x64 tiles interleaved over them (tile t -> device t % n, for
+// image's 32x32 tiles (tile_size overrides) interleaved over them (tile t -> device t % n, for
 // balance: sky rows are cheap), one host thread per device driving its
 // context, and the join is a gather: every device's packed RGB8 tiles are
 // copied to the first device (hipMemcpyPeerAsync: a DMA over xGMI when peer
@@ -99,6 +99,10 @@ int group_create(const int32_t* devices, uint32_t n, zrt_group** out, Make make)
     }
     for (int r : rcs)
         if (r != ZRT_OK) rc = r;
+    if (rc == ZRT_OK)        // repeats of a device render side by side: split its queue budget
+        for (uint32_t i = 0; i < n; ++i)
+            zrt::context_set_mem_share(g->ctx[i], (uint32_t)std::count(g->devices.begin(), g->devices.end(),
+                                                                        g->devices[i]));
     if (rc == ZRT_OK) {
         DevGuard dg(g->devices[0]);
         for (uint32_t i = 1; i < n; ++i) {

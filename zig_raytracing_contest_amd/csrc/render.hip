@@ -7,8 +7,8 @@
 //
 // Organisation (MI355X-first, not the reference's thread blocks):
 //   * a work item is ONE path sample (pixel, sample); items are numbered
-//     pixel-major over this rank's packed pixel list (64x64 tiles walked in
-//     8x8 blocks), item = pixel * S + sample of the pass, so one wave64 of
+//     pixel-major over this rank's packed pixel list (tile_size tiles, 64x64 by
+//     default on one device, walked in 8x8 blocks), item = pixel * S + sample of the pass, so one wave64 of
 //     the primary launch = 64 samples of one pixel (coherent primary rays)
 //     and its records are contiguous;
 //   * bounce k of every path of a pass is one launch over a compacted queue
@@ -1777,6 +1777,7 @@ constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double
 
 struct zrt_context {
     int device = 0;
+    uint32_t mem_share = 1;            // contexts rendering on this device at once (a group's repeats)
     hipStream_t stream = nullptr;
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     std::vector<hipEvent_t> ev_trace;
@@ -2650,7 +2651,7 @@ extern "C" int zrt_context_grid_info(zrt_context* c, zrt_grid* grid, uint32_t in
 // on 2 sets, the last one alone).  The pass count is a multiple of the sets
 // (when spp allows), so the streams stay balanced to the end of the frame.
 static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, uint32_t P, uint32_t sets,
-                             size_t held) {
+                             size_t held, uint32_t share) {
     const uint64_t spp = cfg->num_samples;
     const uint64_t cap = std::max<uint64_t>(1, 0x7FFFFF00ull / P);     // items of a pass < 2^31
     if (cfg->samples_per_pass) return std::min<uint64_t>(std::min<uint64_t>(cfg->samples_per_pass, spp), cap);
@@ -2658,6 +2659,7 @@ static uint64_t pass_samples(const zrt_render_config* cfg, uint64_t per_item, ui
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
         budget = std::min(budget, (free_b + held) / 10 * 6);
+    budget /= std::max<uint32_t>(share, 1u);      // contexts of a group sharing this device
     const uint64_t fit = std::min<uint64_t>(cap, std::max<uint64_t>(1, budget / sets / (per_item * P)));
     uint64_t npass = std::max<uint64_t>(std::min<uint64_t>(sets, spp), (spp + fit - 1) / fit);
     npass = std::min<uint64_t>(spp, (npass + sets - 1) / sets * sets);
@@ -2719,7 +2721,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     for (const zrt_context::PassSet& ps : c->set)
         held += 16ull * (ps.q0_cap + ps.q1_cap + ps.term_cap + ps.stk4_cap + ps.hit_cap) + 8ull * ps.stk2_cap +
                 4ull * ps.wfc_cap;
-    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets, held);
+    const uint64_t s_pass = pass_samples(cfg, per_item, P, counting ? 1u : want_sets, held, c->mem_share);
     const uint32_t npasses = (uint32_t)((spp + s_pass - 1) / s_pass);
     // pass sets: pass p runs on set p % nsets, each set with its own stream
     // and buffers, so one pass's launches fill the machine while another's
@@ -3179,6 +3181,10 @@ extern "C" int zrt_context_profile(const zrt_context* c, zrt_kernel_profile* out
     return ZRT_OK;
 }
 
+void zrt::context_set_mem_share(zrt_context* c, uint32_t share) {
+    if (c) c->mem_share = std::max<uint32_t>(share, 1u);
+}
+
 int zrt::context_device_rgb(const zrt_context* c, const uint8_t** d_rgb, uint32_t* pixels, int* device) {
     if (!c || !d_rgb || !pixels || !device) return ZRT_ERR_INVALID_ARG;
     *d_rgb = c->d_rgb;
@@ -3202,8 +3208,12 @@ extern "C" int zrt_render(const zrt_scene* scene, const zrt_camera* cam, const z
         zrt_group_destroy(g);
         return rc;
     }
+    // a one-entry list names the device (it used to fall back to
+    // cfg->device silently)
+    if (cfg->num_devices == 1 && !cfg->devices) return ZRT_ERR_INVALID_ARG;
+    const int32_t dev = cfg->num_devices == 1 ? cfg->devices[0] : cfg->device;
     zrt_context* c = nullptr;
-    int rc = zrt_context_create(scene, cfg->device, &c);
+    int rc = zrt_context_create(scene, dev, &c);
     if (rc != ZRT_OK) return rc;
     zrt_render_config one = *cfg;
     one.rank = 0;

@@ -55,4 +55,9 @@ int tile_pixels(uint32_t w, uint32_t h, uint32_t tile, uint32_t rank, uint32_t n
 // gathers (group.hip).
 int context_device_rgb(const zrt_context* c, const uint8_t** d_rgb, uint32_t* pixels, int* device);
 
+// Contexts of one group that share a device render at the same time: each
+// sizes its passes from 1/share of the device's queue budget (group.hip sets
+// share = how often the device appears in the list).
+void context_set_mem_share(zrt_context* c, uint32_t share);
+
 }  // namespace zrt

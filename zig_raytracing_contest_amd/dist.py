@@ -2,7 +2,7 @@
 
 SURVEY.md §8e: tiles of the output image shard trivially (the reference
 already splits pixels into independent blocks, stage3.zig:228-229); each rank
-renders the 64x64 tiles t with t % world == rank into a packed RGB8 buffer
+renders the TILE x TILE tiles (32x32) t with t % world == rank into a packed RGB8 buffer
 (zrt_tile_pixels order), then ONE gather moves every rank's packed tiles to
 rank 0 (RCCL over xGMI on GPUs: torch.distributed "nccl"; gloo on CPU for the
 tests), where they are scattered back into the w x h x 3 image.  No reduction:
