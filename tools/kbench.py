@@ -57,6 +57,8 @@ for var in (a.var or [""]):
            "kernel_ms": round(st["trace_kernel_ms"], 2), "wall_ms": round(min(ts) * 1e3, 2),
            "identical": same, "segments": int(st["segments"]),
            "img_sha1": hashlib.sha1(img.tobytes()).hexdigest()[:12]}
+    if flags & native.FLAG_KERNEL_TIMES:   # per-kernel device ms of the last frame (one stream with FLAG_ONE_SET)
+        rec["kernels_ms"] = {k: round(v["ms"], 2) for k, v in ctx.profile()["kernels"].items()}
     if not same:
         dif = np.any(ref != img, axis=2)
         rec["diff_pixels"] = int(dif.sum())
