@@ -991,6 +991,14 @@ constexpr int kParkWaves = kParkBlock / 64;
 // r03za, on the round-3 kernels: 256 vs 128 cfg3 +0.5%, cfg5 +0.4%, cfg2
 // -0.5%; 64 -0.7 / -1.0 / -0.5%)
 constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
+// ZRT_PARK_ADAPT: a launch with few entries per wave (the last bounces, an
+// 8-rank tile set) takes smaller chunks, down to 64, so the waves' last
+// chunks end closer together (the launch tail).  r05e, alternating processes,
+// 2 rounds, images identical: cfg3 5801 / 5810 vs 5765 / 5749 (+0.8%), cfg2
+// +0.6%, cfg5 +0.1% (profiles/r05/r05e_ab_p96_park_adapt.log)
+#ifndef ZRT_PARK_ADAPT
+#define ZRT_PARK_ADAPT 1
+#endif
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
 // a store whose VGPR operands are read late, so whenever the register
@@ -1095,7 +1103,27 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 
 // ESC: with the escape table (context_escape decides per scene)
 template <bool ESC>
-__global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
+// ZRT_PARK_NVGPR / ZRT_SHADE_NVGPR (0: the compiler's choice): VGPR caps that
+// let the shade and primary kernels of one pass set co-reside with the other
+// set's park kernel (512 VGPRs per SIMD lane, allocated in granules of 8: a
+// park kernel at 4 waves x 104 leaves 96, one shade wave of 88)
+#ifndef ZRT_PARK_NVGPR
+#define ZRT_PARK_NVGPR 0
+#endif
+#ifndef ZRT_SHADE_NVGPR
+#define ZRT_SHADE_NVGPR 0
+#endif
+#if ZRT_PARK_NVGPR
+#define ZRT_PARK_ATTR __attribute__((amdgpu_waves_per_eu(512 / ZRT_PARK_NVGPR, 8)))
+#else
+#define ZRT_PARK_ATTR
+#endif
+#if ZRT_SHADE_NVGPR
+#define ZRT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(512 / ZRT_SHADE_NVGPR, 8)))
+#else
+#define ZRT_SHADE_ATTR
+#endif
+__global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
@@ -1130,6 +1158,13 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     bool more = true;
     uint32_t grp = blockIdx.x & 7u, tried = 0;
     uint32_t cb = 0, ce = 0, cgrp = 0;     // the wave's current chunk of queue entries
+    uint32_t chunk = kParkChunk;
+    if (ZRT_PARK_ADAPT) {                  // (wave-uniform: the previous launch's final counts)
+        uint32_t ntot = 0;
+        for (uint32_t g = 0; g < 8u; ++g) ntot += w.n_in8[g * kCtr];
+        const uint32_t per = ntot / (gridDim.x * (blockDim.x >> 6) * 4u);
+        chunk = __builtin_amdgcn_readfirstlane(max(64u, min(kParkChunk, per & ~63u)));
+    }
     // the segment: ray, DDA state, best hit, range
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     DdaV s;                                // grids of <= 1024 cells per axis (zrt_context_render)
@@ -1179,11 +1214,11 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
             while (idle != 0ull && (ce > cb || more)) {
                 if (cb == ce) {
                     uint32_t base = 0, lim = 0;
-                    more = wf_fetch<false>(w, kParkChunk, grp, tried, base, lim);
+                    more = wf_fetch<false>(w, chunk, grp, tried, base, lim);
                     PARK_STAMP(11);
                     if (!more) break;
                     cb = base;
-                    ce = min(base + kParkChunk, lim);
+                    ce = min(base + chunk, lim);
                     cgrp = grp;
                 }
                 const uint32_t take = min((uint32_t)__popcll(idle), ce - cb);
@@ -1558,7 +1593,7 @@ template <bool LMATS>
 #ifndef ZRT_SHADE_MINW
 #define ZRT_SHADE_MINW 1
 #endif
-__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(const WfParams w) {
+__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) ZRT_SHADE_ATTR void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dynm[];    // LMATS: p.nmat DevMat
