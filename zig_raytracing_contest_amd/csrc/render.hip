@@ -58,7 +58,10 @@ constexpr int kTraceThreads = 256;                   // threads per wf_kernel / 
 #define ZRT_TRI_BATCH 2
 #endif
 constexpr int kTriBatch = ZRT_TRI_BATCH;             // triangle loads in flight per lane
-constexpr int kParkBlock = 1024;                     // wf_park_kernel: one workgroup per CU
+#ifndef ZRT_PARK_BLOCK_T
+#define ZRT_PARK_BLOCK_T 1024
+#endif
+constexpr int kParkBlock = ZRT_PARK_BLOCK_T;         // wf_park_kernel: one workgroup per CU
 #ifndef ZRT_SHADE_N
 #define ZRT_SHADE_N 2
 #endif
