@@ -80,6 +80,16 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_TRI36
 #define ZRT_TRI36 0
 #endif
+// ZRT_PLANES16: a scattering hit's bounce-plane record is (albedo, has
+// emissive) in one float4 (16 B, one store) plus a float4 emissive record
+// only when the material emits, against 24 B in two stores (stk4 + stk2):
+// the lamps are the only emissive materials of the stand-in scenes.  r05j,
+// alternating processes, 2 rounds, images identical: cfg3 5894 / 5899 vs
+// 5819 / 5812 (+1.4%), cfg5 +1.0%, cfg2 +1.1%; one-stream resolve 6.1 -> 4.3
+// ms per cfg3 frame (profiles/r05/r05j_ab_planes16.log)
+#ifndef ZRT_PLANES16
+#define ZRT_PLANES16 1
+#endif
 // ZRT_PRIM_SKIP: the primary lane walk crosses empty 4^3 bricks in one
 // BRICK_SKIPV (dda.h) instead of cell by cell (camera rays: ~84% of their
 // cells lie in empty bricks, ~4 cells per brick entered, tools/walk_sim.cpp)
@@ -617,6 +627,8 @@ struct WfParams {
     float4* q_out;
     float4* stk4;             // bounce planes, slot-major: float4 (e, a.x) at [slot * T + item]
     float2* stk2;             //   and float2 (a.y, a.z) at [slot * T + item] (24 B per pair)
+                              // ZRT_PLANES16: stk4 = (a, emissive bits != 0), stk2 = float4 e
+                              // at [slot * T + item], written for emissive hits only
     float4* term;             // [item]: terminal L.xyz, scatter mask bits
     uint32_t T;               // items in this pass
     uint32_t* fetch8;         // work counter per group of this launch
@@ -713,8 +725,17 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
         // (f64, 64-bit RNG) runs without the six colour registers live; 24 B
         // per pair instead of two float4 (r03zk: cfg3 +0.5%, cfg2 +1.6%,
         // cfg5 +1.3%: this write and wf_resolve_kernel's read are HBM-bound)
-        w.stk4[(uint64_t)slot * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, albedo.x);
-        w.stk2[(uint64_t)slot * w.T + item] = make_float2(albedo.y, albedo.z);
+        if (ZRT_PLANES16) {
+            // (a, has_e) in 16 B; e only for emissive hits (its own plane)
+            const uint32_t eb = __float_as_uint(emissive.x) | __float_as_uint(emissive.y) | __float_as_uint(emissive.z);
+            w.stk4[(uint64_t)slot * w.T + item] = make_float4(albedo.x, albedo.y, albedo.z, __uint_as_float(eb));
+            if (eb != 0u)
+                reinterpret_cast<float4*>(w.stk2)[(uint64_t)slot * w.T + item] =
+                    make_float4(emissive.x, emissive.y, emissive.z, 0.0f);
+        } else {
+            w.stk4[(uint64_t)slot * w.T + item] = make_float4(emissive.x, emissive.y, emissive.z, albedo.x);
+            w.stk2[(uint64_t)slot * w.T + item] = make_float2(albedo.y, albedo.z);
+        }
         const float nx = (float)rng_norm64(rng, zx, zf);
         const float ny = (float)rng_norm64(rng, zx, zf);
         const float nz = (float)rng_norm64(rng, zx, zf);
@@ -1791,9 +1812,20 @@ __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(const float4* __rest
                 const uint32_t mask = __float_as_uint(tm.w);
                 for (int slot = (int)max_bounce - 1; slot >= 0; --slot) {
                     if ((mask >> slot) & 1u) {
-                        const float4 e = stk4[(uint64_t)slot * T + item];
-                        const float2 a = stk2[(uint64_t)slot * T + item];
-                        L = add(mk(e.x, e.y, e.z), mul(mk(e.w, a.x, a.y), L));
+                        if (ZRT_PLANES16) {
+                            // e = +0 exactly when the hit stored no emissive plane
+                            const float4 a = stk4[(uint64_t)slot * T + item];
+                            v3 e = mk(0.0f, 0.0f, 0.0f);
+                            if (__float_as_uint(a.w) != 0u) {
+                                const float4 ee = reinterpret_cast<const float4*>(stk2)[(uint64_t)slot * T + item];
+                                e = mk(ee.x, ee.y, ee.z);
+                            }
+                            L = add(e, mul(mk(a.x, a.y, a.z), L));
+                        } else {
+                            const float4 e = stk4[(uint64_t)slot * T + item];
+                            const float2 a = stk2[(uint64_t)slot * T + item];
+                            L = add(mk(e.x, e.y, e.z), mul(mk(e.w, a.x, a.y), L));
+                        }
                     }
                 }
                 float* dst = s_l + i * kResRow + 3u * k;
@@ -2865,9 +2897,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const uint32_t mb = cfg->max_bounce;
     const uint32_t nb = std::max<uint32_t>(mb, 1);
     // per-item bytes of a pass: counting megakernel = the float4 sample
-    // radiance; wavefront = 2 queues x 48 B + terminal 16 B + (e, a) 24 B per
-    // bounce slot (+ the 16 B hit record the park kernel hands the shade kernel)
-    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + 24ull * nb;
+    // radiance; wavefront = 2 queues x 48 B + terminal 16 B + the bounce
+    // planes per slot ((a, has_e) 16 B + e 16 B with ZRT_PLANES16, else 24 B)
+    // (+ the 16 B hit record the park kernel hands the shade kernel)
+    const uint64_t per_item = counting ? 16ull : 96ull + 16ull + 16ull + (ZRT_PLANES16 ? 32ull : 24ull) * nb;
     // small frames run one set: a second stream costs its first launches
     // (the zrt CLI's 3-spp 1080p frame rendered in 30-39 vs 12.5-13.3 ms on a
     // fresh process) and does not pay back (cfg3 at 3 spp, warm: 7.1 vs 6.8
@@ -2921,7 +2954,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grow(&ps.q1, &ps.q1_cap, 3 * T)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.term, &ps.term_cap, T)) != ZRT_OK) return rc;
         if ((rc = grow(&ps.stk4, &ps.stk4_cap, T * nb)) != ZRT_OK) return rc;
-        if ((rc = grow(&ps.stk2, &ps.stk2_cap, T * nb)) != ZRT_OK) return rc;
+        if ((rc = grow(&ps.stk2, &ps.stk2_cap, T * nb * (ZRT_PLANES16 ? 2 : 1))) != ZRT_OK) return rc;
         if ((rc = grow(&ps.wfc, &ps.wfc_cap, 32ull * kCtr * (mb + 2))) != ZRT_OK) return rc;
         if (k == 0) {
             ps.stream = c->stream;
@@ -3015,7 +3048,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             const zrt_context::PassSet& ps = c->set[k];
             bad = shortfall("q0", ps.q0, ps.q0_cap, 3 * T) || shortfall("q1", ps.q1, ps.q1_cap, 3 * T) ||
                   shortfall("term", ps.term, ps.term_cap, T) || shortfall("planes4", ps.stk4, ps.stk4_cap, T * nb) ||
-                  shortfall("planes2", ps.stk2, ps.stk2_cap, T * nb) ||
+                  shortfall("planes2", ps.stk2, ps.stk2_cap, T * nb * (ZRT_PLANES16 ? 2 : 1)) ||
                   shortfall("counters", ps.wfc, ps.wfc_cap, 32ull * kCtr * (mb + 2)) ||
                   (park_next && shortfall("hit records", ps.hit, ps.hit_cap, T)) ||
                   (k > 0 && (!ps.stream || !ps.ev_join));
