@@ -1600,6 +1600,47 @@ __device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx,
                __float_as_uint(b.w) & 0xFFFFu, __float_as_uint(b.w) >> 16, rng, __float_as_uint(c.z), h, tr,
                below, grp, n_seg, sp);
 }
+// ZRT_SHADE_EARLY_APPEND: whether a path continues is known from its records
+// alone (shade_segment: a hit with depth >= 2 continues, whether it scatters
+// or passes through; a miss ends), so the wave reserves its appends with one
+// returning atomic right after the records land and the atomic's latency
+// overlaps the shading chain (triangle data -> texels -> RNG) instead of
+// following it; the path is stored at its reserved position.  r05m,
+// alternating processes, 2 rounds, images identical: cfg3 6019 / 6008 vs 5895
+// / 5877 (+2.2%), cfg5 +0.6%, cfg2 ±0; one-stream shade 23.3-27.0 -> 18.3-18.6
+// ms per cfg3 frame (profiles/r05/r05m_ab_shade_early_append.log)
+#ifndef ZRT_SHADE_EARLY_APPEND
+#define ZRT_SHADE_EARLY_APPEND 1
+#endif
+__device__ __forceinline__ bool shade_continues(bool valid, float4 b, float4 h) {
+    return valid && h.x != kInf && (__float_as_uint(b.w) & 0xFFFFu) >= 2u;
+}
+// One entry (records loaded) shaded: an ending path writes its terminal
+// radiance; a continuing one is left in (o, d, item, depth, slot, rng, mask)
+// for the caller to store at its reserved position.
+struct ShadeOut {
+    v3 o, d;
+    uint32_t item, depth, slot, mask;
+    Rng rng;
+};
+__device__ __forceinline__ void shade_entry_keep(const WfParams& w, const double* zx, const double* zf,
+                                                 const DevMat* mats, bool valid, float4 a, float4 b, float4 c,
+                                                 float4 h, const TriRec& tr, ShadeOut& so, uint32_t& n_seg,
+                                                 unsigned long long* sp = nullptr) {
+    if (!valid) return;
+    so.rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
+    so.item = __float_as_uint(a.w);
+    so.o = mk(a.x, a.y, a.z);
+    so.d = mk(b.x, b.y, b.z);
+    so.depth = __float_as_uint(b.w) & 0xFFFFu;
+    so.slot = __float_as_uint(b.w) >> 16;
+    so.mask = __float_as_uint(c.z);
+    v3 L = mk(0, 0, 0);
+    ++n_seg;
+    if (!shade_segment(w, zx, zf, mats, so.item, h.x, h.y, h.z, tr, so.o, so.d, so.depth, so.slot, so.rng, so.mask,
+                       L, sp))
+        w.term[so.item] = make_float4(L.x, L.y, L.z, __uint_as_float(so.mask));
+}
 // ZRT_SHADE_TRI_EARLY: every entry's triangle Data record is loaded before
 // the first entry is shaded (the second entry's hop hit ->
 // triangle data overlaps the first's hop triangle data -> texels)
@@ -1757,7 +1798,31 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) ZRT_SHADE_ATTR void wf
                 }
             }
         }
-        if (ZRT_SHADE_TRI_EARLY) {
+        if (ZRT_SHADE_EARLY_APPEND && !ZRT_PARK_MISS) {
+            bool pc[kShadeEntries];
+            uint64_t m[kShadeEntries];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int e = 0; e < kShadeEntries; ++e) {
+                pc[e] = shade_continues(hit[e], b[e], h[e]);
+                m[e] = __ballot(pc[e]);
+                tot += (uint32_t)__popcll(m[e]);
+            }
+            uint32_t ob = 0;
+            if (lane == 0 && tot != 0u) ob = atomicAdd(&w.n_out8[grp * kCtr], tot);
+            uint32_t before = 0;
+#pragma unroll
+            for (int e = 0; e < kShadeEntries; ++e) {
+                ShadeOut so;
+                shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
+                                 tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so, n_seg, sp);
+                // (converged again: lane 0's reservation, long returned, reaches every lane)
+                const uint32_t base = __builtin_amdgcn_readfirstlane(ob) + region_base(w, grp) + before;
+                if (pc[e]) q_store(w, base + (uint32_t)__popcll(m[e] & below), so.o, so.d, so.item, so.depth, so.slot,
+                                   so.rng, so.mask);
+                before += (uint32_t)__popcll(m[e]);
+            }
+        } else if (ZRT_SHADE_TRI_EARLY) {
             TriRec tr[kShadeEntries];
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e) tr[e] = tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w));
