@@ -683,7 +683,8 @@ __device__ __forceinline__ uint32_t region_base(const WfParams& w, uint32_t g) {
 #endif
 // The hit triangle's Data record (stage3.zig:199-206: normals, uvs, material),
 // loaded by the caller so that a lane shading several entries can issue every
-// entry's load before the first entry's texel loads (ZRT_SHADE_TRI_EARLY).
+// entry's load before the first entry's texel loads (r05c: -4% shade time
+// alone, but the kernel no longer fits beside the park kernel).
 struct TriRec {
     float4 d0, d1, d2, d3;
 };
@@ -1127,27 +1128,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 
 // ESC: with the escape table (context_escape decides per scene)
 template <bool ESC>
-// ZRT_PARK_NVGPR / ZRT_SHADE_NVGPR (0: the compiler's choice): VGPR caps that
-// let the shade and primary kernels of one pass set co-reside with the other
-// set's park kernel (512 VGPRs per SIMD lane, allocated in granules of 8: a
-// park kernel at 4 waves x 104 leaves 96, one shade wave of 88)
-#ifndef ZRT_PARK_NVGPR
-#define ZRT_PARK_NVGPR 0
-#endif
-#ifndef ZRT_SHADE_NVGPR
-#define ZRT_SHADE_NVGPR 0
-#endif
-#if ZRT_PARK_NVGPR
-#define ZRT_PARK_ATTR __attribute__((amdgpu_waves_per_eu(512 / ZRT_PARK_NVGPR, 8)))
-#else
-#define ZRT_PARK_ATTR
-#endif
-#if ZRT_SHADE_NVGPR
-#define ZRT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(512 / ZRT_SHADE_NVGPR, 8)))
-#else
-#define ZRT_SHADE_ATTR
-#endif
-__global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const WfParams w) {
+__global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
@@ -1474,96 +1455,6 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
 #endif
 }
 
-// ZRT_QSORT: the bounce queue ordered by ray direction within windows
-// (VERDICT r4 #3): after the launch that appends bounce k + 1's paths, one
-// workgroup per window of kQsWin consecutive entries of a region reorders
-// them by the escape table's direction bin (escape.h esc_dir_bin) into the
-// queue the next launch reads.  The paths of a window come from a few
-// neighbouring pixels (pixel-major items, region g = pixel range g), so a
-// park wave's rays then share both origin neighbourhood and direction cone:
-// they walk the same cells side by side.  Queue order is free (every path's
-// records are indexed by its item and slot): same image.
-#ifndef ZRT_QSORT
-#define ZRT_QSORT 0
-#endif
-#ifndef ZRT_QSORT_E
-#define ZRT_QSORT_E 4
-#endif
-#ifndef ZRT_QSORT_BINS
-#define ZRT_QSORT_BINS 4       // bins per face axis: 6 x B x B direction bins
-#endif
-constexpr uint32_t kQsBlock = 1024, kQsE = ZRT_QSORT_E, kQsWin = kQsBlock * kQsE;
-constexpr uint32_t kQsB = ZRT_QSORT_BINS, kQsNBin = 6 * kQsB * kQsB;
-__device__ __forceinline__ uint32_t qsort_bin(float dx, float dy, float dz) {
-    const float ax = fabsf(dx), ay = fabsf(dy), az = fabsf(dz);
-    uint32_t a;
-    float m, u, v;
-    if (ax >= ay && ax >= az) { a = 0; m = dx; const float r = __builtin_amdgcn_rcpf(ax); u = dy * r; v = dz * r; }
-    else if (ay >= az) { a = 1; m = dy; const float r = __builtin_amdgcn_rcpf(ay); u = dx * r; v = dz * r; }
-    else { a = 2; m = dz; const float r = __builtin_amdgcn_rcpf(az); u = dx * r; v = dy * r; }
-    const float fb = (float)kQsB;
-    const uint32_t iu = (uint32_t)fminf(fmaxf((u + 1.0f) * 0.5f * fb, 0.0f), fb - 1.0f);
-    const uint32_t iv = (uint32_t)fminf(fmaxf((v + 1.0f) * 0.5f * fb, 0.0f), fb - 1.0f);
-    // serpentine order inside a face: neighbouring bins stay adjacent
-    const uint32_t ivs = (iu & 1u) ? kQsB - 1u - iv : iv;
-    return ((2u * a + (m < 0.0f ? 1u : 0u)) * kQsB + iu) * kQsB + ivs;
-}
-__global__ __launch_bounds__(kQsBlock) void qsort_kernel(const float4* __restrict__ in, float4* __restrict__ out,
-                                                         const uint32_t* __restrict__ n8, uint32_t P, uint32_t S) {
-    __shared__ uint32_t hist[kQsNBin];
-    const uint32_t g = blockIdx.x & 7u, w0 = (blockIdx.x >> 3) * kQsWin;
-    const uint32_t n = n8[g * kCtr];
-    if (w0 >= n) return;                                    // (uniform over the block)
-    const uint32_t m = min(kQsWin, n - w0);
-    const uint64_t base = (uint64_t)S * xcd_q0(P, g) + w0;
-    for (uint32_t i = threadIdx.x; i < kQsNBin; i += kQsBlock) hist[i] = 0u;
-    __syncthreads();
-    float4 a[kQsE], b[kQsE], c[kQsE];
-    uint32_t bin[kQsE];
-#pragma unroll
-    for (uint32_t e = 0; e < kQsE; ++e) {
-        const uint32_t i = threadIdx.x + e * kQsBlock;
-        bin[e] = ~0u;
-        if (i < m) {
-            a[e] = in[3 * (base + i)];
-            b[e] = in[3 * (base + i) + 1];
-            c[e] = in[3 * (base + i) + 2];
-            bin[e] = qsort_bin(b[e].x, b[e].y, b[e].z);
-            atomicAdd(&hist[bin[e]], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {                                 // exclusive scan of the bins: one wave
-        constexpr uint32_t kPer = (kQsNBin + 63u) / 64u;
-        const uint32_t lane = threadIdx.x;
-        uint32_t loc[kPer], sum = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const uint32_t j = lane * kPer + k;
-            loc[k] = j < kQsNBin ? hist[j] : 0u;
-            sum += loc[k];
-        }
-        uint32_t tot;
-        uint32_t pre = wave_excl_sum(sum, lane, tot);
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const uint32_t j = lane * kPer + k;
-            if (j < kQsNBin) hist[j] = pre;
-            pre += loc[k];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t e = 0; e < kQsE; ++e) {
-        if (bin[e] != ~0u) {
-            const uint64_t dst = base + atomicAdd(&hist[bin[e]], 1u);
-            out[3 * dst] = a[e];
-            out[3 * dst + 1] = b[e];
-            out[3 * dst + 2] = c[e];
-        }
-    }
-}
-
 // Split launches: the shading half of a bounce (traceRayRecursive's body
 // after traceRay, stage3.zig:195-219) over the hit records wf_park_kernel
 // wrote, one lane per path with every lane of the wave busy, appending the
@@ -1641,12 +1532,6 @@ __device__ __forceinline__ void shade_entry_keep(const WfParams& w, const double
                        L, sp))
         w.term[so.item] = make_float4(L.x, L.y, L.z, __uint_as_float(so.mask));
 }
-// ZRT_SHADE_TRI_EARLY: every entry's triangle Data record is loaded before
-// the first entry is shaded (the second entry's hop hit ->
-// triangle data overlaps the first's hop triangle data -> texels)
-#ifndef ZRT_SHADE_TRI_EARLY
-#define ZRT_SHADE_TRI_EARLY 0
-#endif
 
 // LMATS: the material descriptors (at most kLdsMats) copied to dynamic LDS
 // (nmat x 96 B: the shade kernel's LDS stays small, so its workgroups still
@@ -1658,7 +1543,7 @@ template <bool LMATS>
 #ifndef ZRT_SHADE_MINW
 #define ZRT_SHADE_MINW 1
 #endif
-__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) ZRT_SHADE_ATTR void wf_shade_kernel(const WfParams w) {
+__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dynm[];    // LMATS: p.nmat DevMat
@@ -1822,13 +1707,6 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) ZRT_SHADE_ATTR void wf
                                    so.rng, so.mask);
                 before += (uint32_t)__popcll(m[e]);
             }
-        } else if (ZRT_SHADE_TRI_EARLY) {
-            TriRec tr[kShadeEntries];
-#pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) tr[e] = tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w));
-#pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e)
-                shade_entry(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e], tr[e], below, grp, n_seg, sp);
         } else {
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e)
@@ -3300,10 +3178,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? q0 : q1;
                 W.q_out = (k & 1) ? q1 : q0;
-                if (ZRT_QSORT && park_next) {          // q0: appended (unsorted), q1: sorted, read next
-                    W.q_in = q1;
-                    W.q_out = q0;
-                }
                 W.fetch8 = wfc + kCtr * (16 * k);
                 W.n_in8 = wfc + kCtr * (16 * k + 8);
                 W.n_out8 = wfc + kCtr * (16 * (k + 1) + 8);
@@ -3325,15 +3199,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                     HIP_TRY(hipGetLastError());
                     if ((rc = kt_end(sm)) != ZRT_OK) return rc;
                     ++kp.launches[ZRT_KERNEL_SHADE];
-                }
-                if (ZRT_QSORT && park_next && k + 1 < nb) {
-                    // the next bounce's queue by direction within windows
-                    const uint32_t pmax = (uint32_t)(((P + 63u) / 64u + 7u) / 8u * 64u);
-                    const uint64_t wins = ((uint64_t)S * pmax + kQsWin - 1) / kQsWin;
-                    hipLaunchKernelGGL(qsort_kernel, dim3((uint32_t)(8 * wins)), dim3(kQsBlock), 0, sm,
-                                       (const float4*)q0, q1, (const uint32_t*)(wfc + kCtr * (16 * (k + 1) + 8)), P,
-                                       S);
-                    HIP_TRY(hipGetLastError());
                 }
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 ++launches;
