@@ -1016,6 +1016,12 @@ constexpr int kParkWaves = kParkBlock / 64;
 // r03za, on the round-3 kernels: 256 vs 128 cfg3 +0.5%, cfg5 +0.4%, cfg2
 // -0.5%; 64 -0.7 / -1.0 / -0.5%)
 constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
+// ZRT_PARK_LATE_DRAIN (below, the refill round): r05q, 2 rounds, images
+// identical: cfg5 3576 / 3587 vs 3551 / 3553 (+0.8%, park -1%), cfg3 +0.1%,
+// cfg2 +0.5% (profiles/r05/r05q_ab_park_late_drain.log)
+#ifndef ZRT_PARK_LATE_DRAIN
+#define ZRT_PARK_LATE_DRAIN 1
+#endif
 // ZRT_PARK_ADAPT: a launch with few entries per wave (the last bounces, an
 // 8-rank tile set) takes smaller chunks, down to 64, so the waves' last
 // chunks end closer together (the launch tail).  r05e, alternating processes,
@@ -1209,8 +1215,9 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                     }
                     st = kIdle;
                 }
-                __builtin_amdgcn_s_waitcnt(0x3f70);                // vmcnt(0)
+                if (!ZRT_PARK_LATE_DRAIN) __builtin_amdgcn_s_waitcnt(0x3f70);   // vmcnt(0)
             }
+            bool loaded = false;                                   // (wave-uniform)
             PARK_STAMP(10);
             // idle lanes take entries of the wave's chunk [cb, ce) of group
             // cgrp, a new chunk of kParkChunk entries once it is used up: one
@@ -1273,8 +1280,13 @@ __global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
                 }
                 PARK_STAMP(12);
                 cb += take;
+                loaded = loaded || take != 0u;
                 idle = __ballot(st == kIdle);
             }
+            // ZRT_PARK_LATE_DRAIN: the hit-record stores drain with the new
+            // paths' record loads (vector memory completes in order); only a
+            // round that loaded nothing drains them explicitly
+            if (ZRT_PARK_LATE_DRAIN && !loaded) __builtin_amdgcn_s_waitcnt(0x3f70);
             PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
                 if (!more) break;
