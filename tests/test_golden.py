@@ -105,3 +105,38 @@ def test_gpu_reproduces_vector_goldens():
     f = native.probe(native.PROBE_RNG_F32, keys, len(keys), (len(keys), 16))
     z = native.probe(native.PROBE_RNG_NORM, keys, len(keys), (len(keys), 16))
     assert np.array_equal(f, v["rng_f32"]) and np.array_equal(z, v["rng_norm"])
+
+
+def test_frame_goldens_cover_every_benchmarked_config():
+    """tests/golden/frames.json (tools/make_frame_golden.py) holds the whole
+    frames of every config the bench and the configs log quote, made by the
+    current oracle source (regenerate it when zrt_oracle.c changes)."""
+    import hashlib
+    import json
+    with open(os.path.join(GOLD, "frames.json")) as fh:
+        frames = json.load(fh)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "oracle", "zrt_oracle.c"), "rb") as fh:
+        src = hashlib.sha1(fh.read()).hexdigest()
+    for cfg in ("cfg2", "cfg3", "cfg4", "cfg5"):
+        f = frames[cfg]
+        d = scenes.CONFIGS[cfg]
+        assert (f["scene"], f["spp"], f["max_bounce"], f["height"]) == (d["scene"], d["spp"], d["max_bounce"],
+                                                                       d["height"])
+        assert f["oracle_c_sha1"] == src, f"{cfg}: frames.json predates the oracle source"
+        assert len(f["rgb8_sha1"]) == 40 and len(f["linear_sha1"]) == 40 and f["segments"] > 0
+
+
+def test_oracle_reproduces_the_cfg2_frame_golden(oracle_mod):
+    """The whole cfg2 frame (512^2, 64 spp: ~20 s on 8 CPUs) through the
+    same script that made frames.json: its hashes and counters again."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import make_frame_golden
+    with open(os.path.join(GOLD, "frames.json")) as fh:
+        want = json.load(fh)["cfg2"]
+    got = make_frame_golden.frame("cfg2", min(8, len(os.sched_getaffinity(0))))
+    for k in ("rgb8_sha1", "linear_sha1", "segments", "cells_visited", "triangle_tests", "hits"):
+        assert got[k] == want[k], k
