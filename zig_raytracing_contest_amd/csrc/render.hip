@@ -62,8 +62,10 @@ constexpr int kTriBatch = ZRT_TRI_BATCH;             // triangle loads in flight
 #define ZRT_PARK_BLOCK_T 1024
 #endif
 constexpr int kParkBlock = ZRT_PARK_BLOCK_T;         // wf_park_kernel: one workgroup per CU
+// (3 entries since r05t: 113 VGPRs, which fit beside the park kernel at 96,
+// ZRT_PARK_WPE; one-stream shade 18.9 -> 17.1 ms per cfg3 frame)
 #ifndef ZRT_SHADE_N
-#define ZRT_SHADE_N 2
+#define ZRT_SHADE_N 3
 #endif
 constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue entries per lane per fetch
 #ifndef ZRT_WF_CHUNK
@@ -1134,7 +1136,24 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 
 // ESC: with the escape table (context_escape decides per scene)
 template <bool ESC>
-__global__ __launch_bounds__(kParkBlock) void wf_park_kernel(const WfParams w) {
+#ifndef ZRT_SHADE_TRI_EARLY
+#define ZRT_SHADE_TRI_EARLY 0
+#endif
+// ZRT_PARK_WPE: the park kernel compiled for 5 waves per SIMD (at most 96
+// VGPRs; it still runs 4, one 1024-thread workgroup per CU), so 4 x 96 leave
+// 128 VGPRs per SIMD lane for a shade wave of 3 entries per lane (113) or a
+// primary wave (80) of the other pass set.  r05t, 2 rounds, images identical:
+// with ZRT_SHADE_N 3, cfg3 6014 / 6034 vs 6011 / 6017, cfg2 3902 / 3897 vs
+// 3878 / 3838, cfg5 3584 / 3590 vs 3582 / 3594 (profiles/r05/r05t_ab_park96_shade3.log)
+#ifndef ZRT_PARK_WPE
+#define ZRT_PARK_WPE 5
+#endif
+#if ZRT_PARK_WPE
+#define ZRT_PARK_ATTR __attribute__((amdgpu_waves_per_eu(ZRT_PARK_WPE, 8)))
+#else
+#define ZRT_PARK_ATTR
+#endif
+__global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ uint32_t s_rng[kParkWaves * 192];            // LDS-DMA range + face-mask slots
@@ -1708,11 +1727,20 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
             uint32_t ob = 0;
             if (lane == 0 && tot != 0u) ob = atomicAdd(&w.n_out8[grp * kCtr], tot);
             uint32_t before = 0;
+#if ZRT_SHADE_TRI_EARLY
+            TriRec tre[kShadeEntries];
+#pragma unroll
+            for (int e = 0; e < kShadeEntries; ++e) tre[e] = tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w));
+#endif
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e) {
                 ShadeOut so;
+#if ZRT_SHADE_TRI_EARLY
+                shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e], tre[e], so, n_seg, sp);
+#else
                 shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
                                  tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so, n_seg, sp);
+#endif
                 // (converged again: lane 0's reservation, long returned, reaches every lane)
                 const uint32_t base = __builtin_amdgcn_readfirstlane(ob) + region_base(w, grp) + before;
                 if (pc[e]) q_store(w, base + (uint32_t)__popcll(m[e] & below), so.o, so.d, so.item, so.depth, so.slot,
