@@ -132,18 +132,6 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_FF4
 #define ZRT_FF4 1
 #endif
-// ZRT_PARK_MISS: a bounce segment that misses ends in the park kernel
-// (terminal radiance = the sky colour, stage3.zig:195-197), so the shade
-// kernel loads the path records of hits only
-#ifndef ZRT_PARK_MISS
-#define ZRT_PARK_MISS 0
-#endif
-// ZRT_SHADE_PACK (with ZRT_PARK_MISS): the shade kernel packs the hit entries
-// of its fetches densely over the wave (an LDS list per wave) before shading,
-// so every lane of a shading step holds a hit
-#ifndef ZRT_SHADE_PACK
-#define ZRT_SHADE_PACK 0
-#endif
 // DDA steps per park walk trip, every cell's brick lookup in flight at once
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
 // +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
@@ -1205,7 +1193,6 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
     float nearest = kInf, hu = 0.0f, hv = 0.0f;
     uint32_t hidx = 0;
     uint32_t qi = 0;                       // the path's queue entry
-    uint32_t pitem = 0, pmask = 0;         // ZRT_PARK_MISS: its item and scatter mask
     // the ray's escape-table word (byte offset in a brick's kEscWords) and
     // bit; emask 0: the ray never stops early (no table, or a -inf / NaN
     // crossing sequence)
@@ -1228,10 +1215,6 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                 const bool done = st == kDone;
                 if (done) {
                     w.hit[qi] = make_float4(nearest, hu, hv, __uint_as_float(hidx));
-                    if (ZRT_PARK_MISS && nearest == kInf) {   // stage3.zig:195-197: the sky ends the path
-                        const v3 L = env_color(d);
-                        w.term[pitem] = make_float4(L.x, L.y, L.z, __uint_as_float(pmask));
-                    }
                     st = kIdle;
                 }
                 if (!ZRT_PARK_LATE_DRAIN) __builtin_amdgcn_s_waitcnt(0x3f70);   // vmcnt(0)
@@ -1261,10 +1244,6 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                             const float4 qa = w.q_in[3ull * qi], qb = w.q_in[3ull * qi + 1];
                             o = mk(qa.x, qa.y, qa.z);
                             d = mk(qb.x, qb.y, qb.z);
-                            if (ZRT_PARK_MISS) {
-                                pitem = __float_as_uint(qa.w);
-                                pmask = reinterpret_cast<const uint32_t*>(w.q_in + 3ull * qi + 2)[2];
-                            }
                         }
                         {                                          // queued paths have depth >= 1
                             nearest = kInf;
@@ -1609,100 +1588,13 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
     // loaded before the first is shaded, so their latency overlaps the
     // earlier entries' dependent chains (2: cfg3 +1.2%, cfg2 / cfg5 within
     // noise, 112 VGPRs, r02c6)
-    if (ZRT_SHADE_PACK && ZRT_PARK_MISS) {
-        // the wave's hit entries (queue index, region), packed in fetch order
-        constexpr uint32_t kCap = 128u * kShadeEntries;
-        __shared__ uint32_t s_hq[kTraceThreads / 64][kCap];   // launched with kTraceThreads
-        __shared__ uint8_t s_hg[kTraceThreads / 64][kCap];
-        uint32_t* const hq = s_hq[threadIdx.x >> 6];
-        uint8_t* const hg = s_hg[threadIdx.x >> 6];
-        uint32_t nbuf = 0;                     // wave-uniform
-        for (;;) {
-            uint32_t base = 0, lim = 0;
-            const bool got = wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim);
-            SHADE_STAMP(0, base);
-            if (got) {
-#pragma unroll
-                for (int e = 0; e < kShadeEntries; ++e) {
-                    const uint32_t j = base + 64u * e + lane;
-                    const uint32_t i = j < lim ? ent_index<false>(w, grp, j) : 0u;
-                    const float t = j < lim ? w.hit[i].x : kInf;
-                    const bool hit = t != kInf;
-                    n_seg += (j < lim && !hit) ? 1u : 0u;      // the misses' segments (ended by the park kernel)
-                    const uint64_t hm = __ballot(hit);
-                    if (hit) {
-                        const uint32_t pos = nbuf + (uint32_t)__popcll(hm & below);
-                        hq[pos] = i;
-                        hg[pos] = (uint8_t)grp;
-                    }
-                    nbuf += (uint32_t)__popcll(hm);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            while (nbuf >= 64u * kShadeEntries || (!got && nbuf > 0u)) {
-                const uint32_t n = min(nbuf, 64u * kShadeEntries);
-                float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
-                uint32_t g[kShadeEntries];
-                bool ok[kShadeEntries];
-#pragma unroll
-                for (int e = 0; e < kShadeEntries; ++e) {
-                    const uint32_t k = 64u * e + lane;
-                    ok[e] = k < n;
-                    const uint32_t i = ok[e] ? hq[k] : 0u;
-                    g[e] = ok[e] ? hg[k] : 0u;
-                    a[e] = b[e] = c[e] = h[e] = z4;
-                    if (ok[e]) {
-                        h[e] = w.hit[i];
-                        a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2];
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                // the rest moves to the front (fewer than kCap - n entries)
-                for (uint32_t k = lane; k + n < nbuf; k += 64u) {
-                    const uint32_t q = hq[k + n];
-                    const uint8_t gg = hg[k + n];
-                    __builtin_amdgcn_wave_barrier();
-                    hq[k] = q;
-                    hg[k] = gg;
-                }
-                __builtin_amdgcn_wave_barrier();
-                nbuf -= n;
-#pragma unroll
-                for (int e = 0; e < kShadeEntries; ++e)
-                    shade_entry(w, zx, zf, mats, ok[e], a[e], b[e], c[e], h[e],
-                                tri_rec(p, ok[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), below, g[e], n_seg, sp);
-            }
-            if (!got) break;
-        }
-    } else
     for (;;) {
         uint32_t base = 0, lim = 0;
         if (!wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim)) break;
         SHADE_STAMP(0, base);                  // work atomic
         float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
         bool hit[kShadeEntries];
-        if (ZRT_PARK_MISS) {
-            // the park kernel ended the misses: hit records first, then the
-            // path records of the hits (loaded beside their triangle data)
-            uint32_t ie[kShadeEntries];
-#pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) {
-                const uint32_t j = base + 64u * e + lane;
-                ie[e] = j < lim ? ent_index<false>(w, grp, j) : 0u;
-                h[e] = j < lim ? w.hit[ie[e]] : make_float4(kInf, 0.0f, 0.0f, 0.0f);
-            }
-#pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) {
-                const uint32_t j = base + 64u * e + lane;
-                hit[e] = j < lim && h[e].x != kInf;
-                n_seg += (j < lim && !hit[e]) ? 1u : 0u;      // the misses' segments
-                a[e] = b[e] = c[e] = z4;
-                if (hit[e]) {
-                    const uint32_t i = ie[e];
-                    a[e] = w.q_in[3ull * i]; b[e] = w.q_in[3ull * i + 1]; c[e] = w.q_in[3ull * i + 2];
-                }
-            }
-        } else {
+        {
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e) {
                 const uint32_t j = base + 64u * e + lane;
@@ -1714,7 +1606,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
                 }
             }
         }
-        if (ZRT_SHADE_EARLY_APPEND && !ZRT_PARK_MISS) {
+        if (ZRT_SHADE_EARLY_APPEND) {
             bool pc[kShadeEntries];
             uint64_t m[kShadeEntries];
             uint32_t tot = 0;
