@@ -132,6 +132,8 @@ typedef struct zrt_render_config {
 #define ZRT_FLAG_FRUSTUM      0x100u /* the primary launch always uses the frustum bounds (by default
                                         only for frames of 2^23 samples or more, where their build pays);
                                         same image */
+#define ZRT_FLAG_NO_FRUSTUM   0x200u /* the primary launch never uses the frustum bounds (wins over
+                                        ZRT_FLAG_FRUSTUM); same image */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */

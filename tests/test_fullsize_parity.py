@@ -147,3 +147,36 @@ def test_cfg4_on_a_repeated_device_group_whole_frame():
     finally:
         grp.close()
     _check_whole_frame("cfg4", img.reshape(-1, 3), None, st["segments"])
+
+
+# Kernel modes the default schedule does not pick for a config.  A mode
+# changes what the kernels skip (escape table, frustum bounds), how they walk
+# (per lane instead of the park kernel) or how passes overlap (one stream),
+# never the result: each must reproduce the oracle's whole frame.  cfg3 runs
+# with the escape table by default and cfg5 without it (density), so between
+# them both park kernels and the plain primary are pinned at full size.
+MODES = {"escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
+         "no_frustum": native.FLAG_NO_FRUSTUM, "one_set": native.FLAG_ONE_SET,
+         "lane_walk": native.FLAG_LANE_WALK}
+MODE_FRAMES = [(c, m) for c in ("cfg2", "cfg3") for m in MODES] + \
+    [("cfg5", "escape"), ("cfg5", "no_frustum"), ("cfg5", "lane_walk")]
+
+
+@pytest.fixture(scope="module")
+def scene_cache():
+    cache = {}
+    yield cache
+    for rs, _ in cache.values():
+        rs.close()
+
+
+@pytest.mark.parametrize("cfg,mode", MODE_FRAMES)
+def test_benchmark_frame_whole_in_every_kernel_mode(scene_cache, cfg, mode):
+    d = scenes.CONFIGS[cfg]
+    if cfg not in scene_cache:
+        soup = scenes.get_scene(d["scene"])
+        scene_cache[cfg] = (RenderScene(soup, device=0), camera_for(soup, d["camera"], d["width"], d["height"]))
+    rs, cam = scene_cache[cfg]
+    img, res = rs.render(cam, num_samples=d["spp"], max_bounce=d["max_bounce"], linear=True, flags=MODES[mode])
+    _check_whole_frame(cfg, img.reshape(-1, 3), _row_major(res["linear"], cam.w, cam.h),
+                       res["stats"]["segments"])

@@ -23,6 +23,15 @@ def test_abi_exports_every_declared_symbol():
     assert set(native.EXPORTS) <= declared
 
 
+def test_render_flags_match_the_header():
+    """Every ZRT_FLAG_* of zrt.h has its native.FLAG_* twin with the same bit."""
+    hdr = open(f"{ROOT}/include/zrt.h").read()
+    flags = dict(re.findall(r"#define ZRT_FLAG_([A-Z_]+)\s+(0x[0-9a-fA-F]+)u", hdr))
+    assert "NO_FRUSTUM" in flags and len(flags) >= 8, flags
+    for name, val in flags.items():
+        assert getattr(native, "FLAG_" + name) == int(val, 16), name
+
+
 def test_render_config_layout_is_abi_stable():
     """ABI 2 took the device list out of the reserved words: same size and
     offsets of every ABI-1 field."""

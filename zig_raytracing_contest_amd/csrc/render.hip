@@ -3038,7 +3038,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // block, r04fk3; 0.42 ms one thread per block) and save ~18% of the
     // primary launch: frames of 2^23 samples or more (a 3-spp 1080p frame's
     // primary takes ~0.5 ms: break-even)
-    if (ZRT_FRUSTUM && c->d_sat && !counting && packed &&
+    if (ZRT_FRUSTUM && c->d_sat && !counting && packed && !(cfg->flags & ZRT_FLAG_NO_FRUSTUM) &&
         ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
         // timed region: 32 K threads for a 1080p frame)

@@ -21,7 +21,7 @@ STATUS = {0: "ok", -1: "invalid argument", -2: "no HIP device", -3: "HIP runtime
           -7: "parse error", -8: "not found", -9: "camera/output size rules violated"}
 FLAG_COUNT_STATS, FLAG_LANE_WALK = 0x1, 0x2
 FLAG_ESCAPE, FLAG_NO_ESCAPE = 0x40, 0x80
-FLAG_FRUSTUM = 0x100
+FLAG_FRUSTUM, FLAG_NO_FRUSTUM = 0x100, 0x200
 FLAG_ONE_SET, FLAG_KERNEL_TIMES = 0x10, 0x20
 # zrt_kernel_profile classes (include/zrt.h)
 KERNEL_CLASSES = ("primary", "park", "shade", "bounce", "resolve", "count")
