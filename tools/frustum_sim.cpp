@@ -5,7 +5,8 @@
 // exited below lo (the fast-forward's share) and after the exit that passes
 // hi (the far stop's share), and whether any occupied cell lies past hi.
 //   g++ -O2 -std=c++17 -fopenmp -ffp-contract=off -Izig_raytracing_contest_amd/csrc -Iinclude tools/frustum_sim.cpp -o /tmp/frustum_sim
-//   frustum_sim <scene.bin> <cam.bin> [rays=50000]
+//   frustum_sim <scene.bin> <cam.bin> [rays=50000] [block=8]
+// (block: the pixel block edge of the bounds; the product's is 8)
 // scene.bin: as tools/walk_sim.cpp; cam.bin: origin, lower_left_corner, right,
 // up (3 f32 each), w, h (f32).
 #include <cstdio>
@@ -21,6 +22,7 @@ using namespace zrt;
 int main(int argc, char** argv) {
     if (argc < 3) return 2;
     const int nrays = argc > 3 ? atoi(argv[3]) : 50000;
+    const uint32_t B = argc > 4 ? (uint32_t)atoi(argv[4]) : 8u;
     FILE* f = fopen(argv[1], "rb");
     float bmin[3], bmax[3], cs[3];
     uint32_t res[3], ncells, nrefs;
@@ -54,13 +56,13 @@ int main(int argc, char** argv) {
         for (uint32_t y = 0; y < n1; ++y)
             for (uint32_t x = 0; x < n0; ++x) sat[((size_t)z * n1 + y) * n0 + x] += sat[((size_t)(z - 1) * n1 + y) * n0 + x];
     const EscSat S{sat.data(), n0, n0 * n1};
-    const uint32_t nbx = (W + 7) / 8, nby = (H + 7) / 8;
+    const uint32_t nbx = (W + B - 1) / B, nby = (H + B - 1) / B;
     std::vector<FrustumBound> fb(nbx * nby);
 #pragma omp parallel for
     for (int b = 0; b < (int)(nbx * nby); ++b) {
         const uint32_t bx = b % nbx, by = b / nbx;
-        fb[b] = frustum_bound(S, res, bmin, bmax, cs, cam, cam + 3, cam + 6, cam + 9, 8.0 * bx, 8.0 * bx + 8.0,
-                              8.0 * by, 8.0 * by + 8.0);
+        fb[b] = frustum_bound(S, res, bmin, bmax, cs, cam, cam + 3, cam + 6, cam + 9, (double)B * bx,
+                              (double)B * bx + B, (double)B * by, (double)B * by + B);
     }
     const GridK g{res[0] - 1, res[1] - 1, res[2] - 1, res[0], res[0] * res[1]};
     const v3 o = mk(cam[0], cam[1], cam[2]), llc = mk(cam[3], cam[4], cam[5]), right = mk(cam[6], cam[7], cam[8]),
@@ -73,7 +75,7 @@ int main(int argc, char** argv) {
         const uint32_t px = rng() % W, py = rng() % H;
         const float ux = px + U(rng), vy = py + U(rng);
         const v3 d = normalize(add(add(llc, scale(right, ux)), scale(up, vy)));
-        const FrustumBound b = fb[(py / 8) * nbx + px / 8];
+        const FrustumBound b = fb[(py / B) * nbx + px / B];
         Dda s;
         if (!dda_init(bmin, bmax, res, cs, o, d, s)) continue;
         ++rays;

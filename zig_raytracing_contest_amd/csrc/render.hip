@@ -135,6 +135,12 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // DDA steps per park walk trip, every cell's brick lookup in flight at once
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
 // +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
+// primary frustum bounds per (1 << ZRT_FRUSTUM_SHIFT)^2 pixel block
+#ifndef ZRT_FRUSTUM_SHIFT
+#define ZRT_FRUSTUM_SHIFT 3
+#endif
+constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
+constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
@@ -468,7 +474,7 @@ __device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, 
     const uint32_t pixel = p.pixlist[q];
     const uint32_t py = pixel / p.w;
     const uint32_t px = pixel - py * p.w;
-    if (block) *block = (py >> 3) * p.tlo_nbx + (px >> 3);
+    if (block) *block = (py >> kFrustShift) * p.tlo_nbx + (px >> kFrustShift);
     rng.s = path_key(p.seed, pixel, p.s0 + s_local);
     const float jx = rng_float(rng);
     const float jy = rng_float(rng);
@@ -2363,8 +2369,8 @@ __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restr
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= a.nbx * a.nby) return;
     const uint32_t bx = b % a.nbx, by = b / a.nbx;
-    const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx,
-                                          8.0 * bx + 8.0, 8.0 * by, 8.0 * by + 8.0);
+    const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, kFrustB * bx,
+                                          kFrustB * bx + kFrustB, kFrustB * by, kFrustB * by + kFrustB);
     tlo[b] = make_float4(fb.lo, fb.hi, fb.ga, fb.gb);
 #else
     // one wave per block: lane l tests slices l, l + 64, ... of the same
@@ -2375,8 +2381,8 @@ __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restr
     const uint32_t b = (blockIdx.x * kBlock + threadIdx.x) >> 6;
     if (b >= a.nbx * a.nby) return;                        // (uniform over the wave)
     const uint32_t bx = b % a.nbx, by = b / a.nbx;
-    const FrustumCone q = frustum_cone(a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, 8.0 * bx, 8.0 * bx + 8.0,
-                                       8.0 * by, 8.0 * by + 8.0);
+    const FrustumCone q = frustum_cone(a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, kFrustB * bx,
+                                       kFrustB * bx + kFrustB, kFrustB * by, kFrustB * by + kFrustB);
     int first = 1 << 30, last = -1;
     if (q.ok)
         for (int it = (int)lane; it < (1 << 16) && !(it * q.ds > q.s_far); it += 64)
@@ -3042,7 +3048,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
         // timed region: 32 K threads for a 1080p frame)
-        const uint32_t nbx = (cam->w + 7u) / 8u, nby = (cam->h + 7u) / 8u;
+        const uint32_t nbx = (cam->w + (1u << kFrustShift) - 1u) >> kFrustShift;
+        const uint32_t nby = (cam->h + (1u << kFrustShift) - 1u) >> kFrustShift;
         if ((rc = grow(&c->d_tlo, &c->tlo_cap, (size_t)nbx * nby)) != ZRT_OK) return rc;
         FrustumArgs fa;
         for (int k = 0; k < 3; ++k) {
