@@ -75,13 +75,9 @@ constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue e
 // cfg2 +0.9%, cfg5 +0.2%; 4: +0.6 / +0.5 / 0%)
 constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 
-// Triangle positions per ref (bakeInto's Pos: v0, e1 = v1 - v0, e2 = v2 - v0).
-// ZRT_TRI36: 9 floats (36 B) per ref, read as two dword-aligned 16-byte loads
-// and one dword; otherwise 3 float4 (48 B, w unused).  A cell's refs are
-// contiguous, so 36 B touches 25% fewer cache lines per cell.
-#ifndef ZRT_TRI36
-#define ZRT_TRI36 0
-#endif
+// Triangle positions per ref (bakeInto's Pos: v0, e1 = v1 - v0, e2 = v2 - v0)
+// as 3 float4 (48 B, w unused).  36-byte records touch 25% fewer cache lines
+// per cell but cost the park kernel 9 VGPRs (r05f: cfg3 -9%).
 // ZRT_PLANES16: a scattering hit's bounce-plane record is (albedo, has
 // emissive) in one float4 (16 B, one store) plus a float4 emissive record
 // only when the material emits, against 24 B in two stores (stk4 + stk2):
@@ -92,23 +88,10 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_PLANES16
 #define ZRT_PLANES16 1
 #endif
-// ZRT_PRIM_SKIP: the primary lane walk crosses empty 4^3 bricks in one
-// BRICK_SKIPV (dda.h) instead of cell by cell (camera rays: ~84% of their
-// cells lie in empty bricks, ~4 cells per brick entered, tools/walk_sim.cpp)
-#ifndef ZRT_PRIM_SKIP
-#define ZRT_PRIM_SKIP 0
-#endif
 // ZRT_ESCAPE: the park walk stops a segment once its escape-table bit
 // (escape.h) says every later cell of its ray is empty
 #ifndef ZRT_ESCAPE
 #define ZRT_ESCAPE 1
-#endif
-// (measurement variants: queries without the check / the check without queries)
-#ifndef ZRT_ESC_NOCHECK
-#define ZRT_ESC_NOCHECK 0
-#endif
-#ifndef ZRT_ESC_NODMA
-#define ZRT_ESC_NODMA 0
 #endif
 // ZRT_FRUSTUM: the primary walk fast-forwards (DDAV_FF) over the crossings
 // below its pixel block's frustum bound (escape.h frustum_bound lo); with
@@ -119,18 +102,6 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #endif
 #ifndef ZRT_FRUSTUM_HI
 #define ZRT_FRUSTUM_HI 1
-#endif
-// ZRT_FRUSTUM_GAP: a walk entering a cell inside the block's empty gap
-// (escape.h frustum_bound ga, gb) fast-forwards to gb (r04v: neutral, cfg3
-// 5756 vs 5756 Mrays/s, cfg5 / cfg2 within noise; off)
-#ifndef ZRT_FRUSTUM_GAP
-#define ZRT_FRUSTUM_GAP 0
-#endif
-// ZRT_FF4: the fast-forward as DDAV_FF4 (four branch-free crossings per loop
-// trip; r04s, full spp: cfg3 5730 vs 5695 Mrays/s with DDAV_FF, 5419 without
-// the bounds; cfg5 and cfg2 equal), 2: DDAV_FFC, 0: DDAV_FF
-#ifndef ZRT_FF4
-#define ZRT_FF4 1
 #endif
 // DDA steps per park walk trip, every cell's brick lookup in flight at once
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
@@ -144,9 +115,7 @@ constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
-constexpr uint32_t kTriFloats = ZRT_TRI36 ? 9u : 12u;
-struct Tri { float4 a, b; float c; };   // v0.xyz e1.x | e1.yz e2.xy | e2.z  (TRI36), else a = v0, b = e1, c unused
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+constexpr uint32_t kTriFloats = 12u;
 
 struct TraceParams {
     float bmin[3], bmax[3];
@@ -162,7 +131,7 @@ struct TraceParams {
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
     // primary launch: per 8x8 pixel block of the image (row-major, tlo_nbx
-    // blocks per row) the frustum bounds (lo, hi, ga, gb) of escape.h
+    // blocks per row) the frustum bounds (lo, hi, unused, unused) of escape.h
     // frustum_bound, or null
     const float4* tlo;
     uint32_t tlo_nbx;
@@ -192,15 +161,9 @@ struct TraceParams {
 // Ref j's v0, e1, e2.
 __device__ __forceinline__ void load_tri(const TraceParams& p, uint32_t j, v3& v0, v3& e1, v3& e2) {
     const float* q = p.tri_pos + (uint64_t)kTriFloats * j;
-    if constexpr (ZRT_TRI36) {
-        const f4u a = *reinterpret_cast<const f4u*>(q), b = *reinterpret_cast<const f4u*>(q + 4);
-        const float c = q[8];
-        v0 = mk(a.x, a.y, a.z); e1 = mk(a.w, b.x, b.y); e2 = mk(b.z, b.w, c);
-    } else {
-        const float4 a = *reinterpret_cast<const float4*>(q), b = *reinterpret_cast<const float4*>(q + 4),
-                     c = *reinterpret_cast<const float4*>(q + 8);
-        v0 = mk(a.x, a.y, a.z); e1 = mk(b.x, b.y, b.z); e2 = mk(c.x, c.y, c.z);
-    }
+    const float4 a = *reinterpret_cast<const float4*>(q), b = *reinterpret_cast<const float4*>(q + 4),
+                 c = *reinterpret_cast<const float4*>(q + 8);
+    v0 = mk(a.x, a.y, a.z); e1 = mk(b.x, b.y, b.z); e2 = mk(c.x, c.y, c.z);
 }
 
 // Per-bounce (emissive, albedo) pairs of one path (counting megakernel only).
@@ -312,8 +275,7 @@ template <bool STATS, int TB, bool PACKED = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr,
-                                           float tau = 0.0f, float tfar = kInf, float ga = kInf,
-                                           float gb = kInf) {
+                                           float tau = 0.0f, float tfar = kInf) {
     float nearest = kInf;
     Dda s0;
     if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
@@ -336,18 +298,16 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             if (tau == kInf) return nearest;               // no occupied cell on the ray: the miss
             if (tau > fminf(s.tn0, fminf(s.tn1, s.tn2))) {
                 bool exited;
-                if (ZRT_FF4 == 2) DDAV_FFC(s, p.pk, f0, f1, f2, tau, exited);
-                else if (ZRT_FF4) DDAV_FF4(s, f0, f1, f2, tau, exited);
-                else DDAV_FF(s, f0, f1, f2, tau, exited);
+                // (four branch-free crossings per loop trip: r04s, cfg3 5730 vs
+                // 5695 Mrays/s with one per trip, DDAV_FF)
+                DDAV_FF4(s, f0, f1, f2, tau, exited);
                 if (exited) return nearest;
             }
         }
         bool occupied = brick_occupied_v(p, occ, s.pc);
-        const bool skip_ok = ZRT_PRIM_SKIP && s0.neg < 8u;
         // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
         // bound) the t past which every cell of the ray is empty
         float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
-        if (s0.neg >= 8u) ga = kInf;                       // (the gap fast-forward: see below)
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
@@ -358,28 +318,8 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             float tc;
             PackK pkl = p.pk;
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
-            if (skip_ok && !occupied) {
-                // the cells left in this empty 4^3 brick at once (a 4^3 part
-                // of a larger empty occupancy brick is empty too)
-                BRICK_SKIPV(s, pkl, exited, tc);
-                crossed = true;
-            } else {
-                DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
-            }
+            DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
-            if (ZRT_FRUSTUM_GAP && tc >= ga) {
-                // the cell just entered lies in the block's empty gap: the
-                // crossings below gb enter empty cells, and with lim >= gb no
-                // stop test fires among them (the walk's state after them)
-                ga = kInf;
-                if (lim >= gb) {
-                    if (ZRT_FF4 == 2) DDAV_FFC(s, p.pk, f0, f1, f2, gb, exited);
-                    else if (ZRT_FF4) DDAV_FF4(s, f0, f1, f2, gb, exited);
-                    else DDAV_FF(s, f0, f1, f2, gb, exited);
-                    if (exited) break;
-                    crossed = true;
-                }
-            }
             if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
         }
         return nearest;
@@ -876,7 +816,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             // mask) is re-read after the walk, so it holds no VGPRs in it
             v3 o, d;
             uint32_t depth;
-            float tau = 0.0f, tfar = kInf, ga = kInf, gb = kInf;
+            float tau = 0.0f, tfar = kInf;
             if (PRIMARY) {
                 Rng rng0;
                 uint32_t blk = 0;
@@ -885,8 +825,6 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
                     const float4 fb = p.tlo[blk];
                     tau = fb.x;
                     tfar = fb.y;
-                    ga = fb.z;
-                    gb = fb.w;
                 }
                 depth = p.max_bounce;
             } else {
@@ -900,7 +838,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             WF_STAMP(2);
             if (depth != 0)
                 t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
-                                                        tau, tfar, ga, gb);
+                                                        tau, tfar);
             WF_STAMP(0);
             uint32_t item, slot;
             Rng rng;
@@ -1128,11 +1066,6 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 #define PARK_COUNT(k, v) do { } while (0)
 #endif
 
-// ESC: with the escape table (context_escape decides per scene)
-template <bool ESC>
-#ifndef ZRT_SHADE_TRI_EARLY
-#define ZRT_SHADE_TRI_EARLY 0
-#endif
 // ZRT_PARK_WPE: the park kernel compiled for 5 waves per SIMD (at most 96
 // VGPRs; it still runs 4, one 1024-thread workgroup per CU), so 4 x 96 leave
 // 128 VGPRs per SIMD lane for a shade wave of 3 entries per lane (113) or a
@@ -1147,6 +1080,8 @@ template <bool ESC>
 #else
 #define ZRT_PARK_ATTR
 #endif
+// ESC: with the escape table (context_escape decides per scene)
+template <bool ESC>
 __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -1382,11 +1317,11 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                     // trip cannot have parked the lane: escape.h)
                     const LaneM esc = lm_and(lm_of(st == kWalk), lm_of(ew != 0u));
                     PARK_COUNT(16, __popcll(esc));
-                    if (!ZRT_ESC_NOCHECK) st = lm_selu(esc, kDone, st);
+                    st = lm_selu(esc, kDone, st);
                     // one query per brick the ray enters (its word does not
                     // change while the lane walks inside the brick)
                     const uint32_t b = occx_brick(w, s);
-                    if (!ZRT_ESC_NODMA && st == kWalk && emask != 0u && b != eb) {
+                    if (st == kWalk && emask != 0u && b != eb) {
                         park_load_esc(reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(w.esc) +
                                                                         b * (4u * kEscWords) + eoff),
                                       esc_slot);
@@ -1625,20 +1560,13 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
             uint32_t ob = 0;
             if (lane == 0 && tot != 0u) ob = atomicAdd(&w.n_out8[grp * kCtr], tot);
             uint32_t before = 0;
-#if ZRT_SHADE_TRI_EARLY
-            TriRec tre[kShadeEntries];
-#pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) tre[e] = tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w));
-#endif
+            // (each entry's triangle record loaded as its shading starts: all
+            // of them up front took 100 VGPRs and lost co-residency, r05c)
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e) {
                 ShadeOut so;
-#if ZRT_SHADE_TRI_EARLY
-                shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e], tre[e], so, n_seg, sp);
-#else
                 shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
                                  tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so, n_seg, sp);
-#endif
                 // (converged again: lane 0's reservation, long returned, reaches every lane)
                 const uint32_t base = __builtin_amdgcn_readfirstlane(ob) + region_base(w, grp) + before;
                 if (pc[e]) q_store(w, base + (uint32_t)__popcll(m[e] & below), so.o, so.d, so.item, so.depth, so.slot,
@@ -2074,16 +2002,6 @@ __global__ __launch_bounds__(1024) void occx_pack_kernel(const uint32_t* __restr
 
 }  // namespace
 
-// 3 float4 per ref (the device bake's layout) -> kTriFloats = 9 floats per ref.
-__global__ __launch_bounds__(kBlock) void tri_repack_kernel(const float4* __restrict__ in, uint32_t refs,
-                                                           float* __restrict__ out) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= refs) return;
-    const float4 a = in[3ull * i], b = in[3ull * i + 1], c = in[3ull * i + 2];
-    float* o = out + 9ull * i;
-    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = b.x; o[4] = b.y; o[5] = b.z; o[6] = c.x; o[7] = c.y; o[8] = c.z;
-}
-
 static int context_base(zrt_context* c) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&c->ev_begin));
@@ -2099,7 +2017,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells);
 
 // Word i of ref k's (v0, e1, e2) in the context's triangle layout.
 __device__ __forceinline__ uint32_t tri_word(const float* pos, uint32_t k, uint32_t i) {
-    return __float_as_uint(pos[(uint64_t)kTriFloats * k + (kTriFloats == 9 ? i : i + i / 3)]);
+    return __float_as_uint(pos[(uint64_t)kTriFloats * k + i + i / 3]);
 }
 __device__ __forceinline__ bool same_tri(const float* pos, uint32_t a, uint32_t b) {
     for (uint32_t i = 0; i < 9; ++i)
@@ -2203,11 +2121,7 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     for (uint32_t i = 0; i < c->nrefs; ++i) {
         const float* q = s->triangles_pos + 9ull * i;
         float* o = pos.data() + (size_t)kTriFloats * i;
-        if (kTriFloats == 9) {
-            memcpy(o, q, 36);
-        } else {
-            memcpy(o, q, 12); memcpy(o + 4, q + 3, 12); memcpy(o + 8, q + 6, 12);
-        }
+        memcpy(o, q, 12); memcpy(o + 4, q + 3, 12); memcpy(o + 8, q + 6, 12);
         float tmp[16];
         memcpy(tmp, s->triangles_data + 15ull * i, 15 * sizeof(float));
         memcpy(&tmp[15], &s->triangles_material[i], 4);
@@ -2364,15 +2278,6 @@ struct FrustumArgs {
 __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
                                                          float4* __restrict__ tlo) {
     const EscSat S{sat, a.res[0] + 1u, (a.res[0] + 1u) * (a.res[1] + 1u)};
-#if ZRT_FRUSTUM_GAP
-    // one thread per block: frustum_bound's serial march (the gap needs it)
-    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    if (b >= a.nbx * a.nby) return;
-    const uint32_t bx = b % a.nbx, by = b / a.nbx;
-    const FrustumBound fb = frustum_bound(S, a.res, a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, kFrustB * bx,
-                                          kFrustB * bx + kFrustB, kFrustB * by, kFrustB * by + kFrustB);
-    tlo[b] = make_float4(fb.lo, fb.hi, fb.ga, fb.gb);
-#else
     // one wave per block: lane l tests slices l, l + 64, ... of the same
     // march (frustum_cone / frustum_slice), the wave takes the first and
     // last occupied ones (a 1080p frame: 32 K waves of ~4 slices per lane
@@ -2400,7 +2305,6 @@ __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restr
         if (q.ok) frustum_finish(q, first == (1 << 30) ? -1 : first, last, fb);
         tlo[b] = make_float4(fb.lo, fb.hi, kInf, kInf);
     }
-#endif
 }
 
 // The summed-area table of cell occupancy (escape.h EscSat): kept in the
@@ -2648,22 +2552,7 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
             c->nrefs = dg.refs;
             c->d_cells = dg.cells;
             c->d_data = dg.data;               // the context owns both from here (freed by destroy)
-            if (kTriFloats == 12) {
-                c->d_pos = reinterpret_cast<float*>(dg.pos);
-            } else {   // the device bake writes 3 float4 per ref: repack to 9 floats
-                auto repack = [&]() -> int {
-                    HIP_TRY(hipMalloc((void**)&c->d_pos, 36ull * std::max<uint32_t>(dg.refs, 1)));
-                    if (dg.refs) {
-                        hipLaunchKernelGGL(tri_repack_kernel, dim3((dg.refs + kBlock - 1) / kBlock), dim3(kBlock),
-                                           0, c->stream, (const float4*)dg.pos, dg.refs, c->d_pos);
-                        HIP_TRY(hipGetLastError());
-                        HIP_TRY(hipStreamSynchronize(c->stream));
-                    }
-                    return ZRT_OK;
-                };
-                rc = repack();
-                (void)hipFree(dg.pos);         // on every path: the context never owned it
-            }
+            c->d_pos = reinterpret_cast<float*>(dg.pos);   // the device bake's 3 float4 per ref
             if (rc == ZRT_OK && (rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
         }
     }
@@ -3063,7 +2952,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             fa.up[k] = cam->up[k];
         }
         fa.w = cam->w; fa.h = cam->h; fa.nbx = nbx; fa.nby = nby;
-        const uint64_t fthreads = (uint64_t)nbx * nby * (ZRT_FRUSTUM_GAP ? 1u : 64u);
+        const uint64_t fthreads = (uint64_t)nbx * nby * 64u;
         hipLaunchKernelGGL(frustum_kernel, dim3((uint32_t)((fthreads + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                            (const uint32_t*)c->d_sat, fa, c->d_tlo);
         HIP_TRY(hipGetLastError());
