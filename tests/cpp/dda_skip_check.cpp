@@ -15,6 +15,12 @@
 
 using namespace zrt;
 
+// PK_BM_TEST=1: the brick-major packed words (dda.h; the step macros name PK_BM)
+#ifndef PK_BM_TEST
+#define PK_BM_TEST 0
+#endif
+constexpr bool PK_BM = PK_BM_TEST != 0;
+
 struct TestGrid {
     float bmin[3], bmax[3], cs[3];
     uint32_t res[3];
@@ -68,8 +74,11 @@ static void walk_w(const GridK& k, Dda s) {
     ddaw_from(s, k, w);
     const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
     PackK pk;
-    const bool packs = pack_layout(res, pk);
-    if (!packs) { ++g_walk_fails; return; }
+    const bool packs = pack_layout(res, pk, PK_BM);
+    if (!packs || pk.bm != (uint32_t)PK_BM) {    // (brick-major words pack power-of-two grids only)
+        if (!PK_BM) ++g_walk_fails;
+        return;
+    }
     const bool linear = pack_is_linear(res, pk);
     DdaV x;
     ddav_from(s, k, pk, x);
@@ -159,13 +168,13 @@ static uint64_t g_skipv_fails = 0, g_skipv = 0;
 static void walk_skipv(const TestGrid& g, const GridK& k, const Dda& s0, const std::vector<Rec>& ref) {
     const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
     PackK pk;
-    if (!pack_layout(res, pk)) return;
+    if (!pack_layout(res, pk, PK_BM) || pk.bm != (uint32_t)PK_BM) return;
     DdaV x;
     ddav_from(s0, k, pk, x);
     Dda q = s0;                                   // the cell walk alongside
     size_t n = 0;
     for (int guard = 0; guard < 100000; ++guard) {
-        const uint32_t c0 = x.pc & pk.f0, c1 = (x.pc & pk.f1) >> pk.o1, c2 = (x.pc & pk.f2) >> pk.o2;
+        const uint32_t c0 = pack_coord(pk, x.pc, 0), c1 = pack_coord(pk, x.pc, 1), c2 = pack_coord(pk, x.pc, 2);
         const bool occ = g.occupied(c0, c1, c2);
         if (occ) {
             if (n >= ref.size() || ref[n].c0 != c0 || ref[n].c1 != c1 || ref[n].c2 != c2 ||
@@ -215,7 +224,7 @@ static uint64_t g_ff_fails = 0, g_ff = 0, g_ff_steps = 0;
 static void walk_ff(const GridK& k, const Dda& s0, std::mt19937_64& rng) {
     const uint32_t res[3] = {k.rm0 + 1, k.rm1 + 1, k.rm2 + 1};
     PackK pk;
-    if (!pack_layout(res, pk) || s0.neg >= 8u) return;
+    if (!pack_layout(res, pk, PK_BM) || pk.bm != (uint32_t)PK_BM || s0.neg >= 8u) return;
     Dda q = s0;
     for (int guard = 0; guard < 100000; ++guard) {
         if (rng() % 3 == 0) {                       // fast-forward from here
@@ -278,6 +287,7 @@ int main(int argc, char** argv) {
         const bool pow2 = gi % 3 == 0;     // exact arithmetic -> many crossing ties
         for (int a = 0; a < 3; ++a) {
             g.res[a] = gi == 0 ? 128u : 1u + (uint32_t)(rng() % 40);
+            if (PK_BM && gi % 2 == 1) g.res[a] = 4u << (rng() % 5);   // (grids the brick-major words pack)
             g.bmin[a] = pow2 ? 0.0f : -5.0f + 10.0f * U(rng);
             g.cs[a] = pow2 ? 0.25f : 0.05f + U(rng);
             g.bmax[a] = g.bmin[a] + g.cs[a] * (float)g.res[a];

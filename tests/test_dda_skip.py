@@ -14,9 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
-def test_brick_skip_matches_cell_walk(tmp_path):
+@pytest.mark.parametrize("bm", [0, 1])
+def test_brick_skip_matches_cell_walk(tmp_path, bm):
+    """bm = 1: the same checks on brick-major packed words (power-of-two grids;
+    the kernels' layout for them since r05ag)."""
     exe = tmp_path / "ddachk"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-DPK_BM_TEST={bm}",
                     "-I", os.path.join(ROOT, "zig_raytracing_contest_amd", "csrc"),
                     "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "cpp", "dda_skip_check.cpp"), "-o", str(exe)],

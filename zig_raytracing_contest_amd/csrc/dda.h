@@ -178,12 +178,22 @@ ZHD void ddaw_from(const Dda& d, const GridK& g, DdaW& w) {
 // (tests/cpp/dda_skip_check.cpp, step by step on random grids).  A step past
 // the exit (T_EXIT = +inf) may carry into the next field; the walk ends there
 // (the park kernel's speculative second step only reads a clamped brick).
+// Brick-major words (bm = 1; grids of 4 to 1024 cells per axis, powers of
+// two): bits [0, 6) hold every axis's low two bits (x | y << 2 | z << 4, the
+// cell's index inside its 4^3 brick) and the fields' high parts follow (x
+// from bit 6, y from o1, z from o2), so the word >> 6 is the brick's linear
+// index and its low six bits the in-brick index (no multiply, no field
+// extracts: 8 VALU less per OccX lookup).  A field is then two bit runs, and
+// a step adds +-lowbit(f_a) across the gap (pk_add: 3 VALU more per step).
+// The kernels take the layout as a template parameter (PK_BM, which the step
+// macros below name).
 struct PackK {
-    uint32_t o1, o2;          // bit offsets of fields 1 and 2 (field 0 at bit 0)
+    uint32_t o1, o2;          // bit offsets of fields 1 and 2 (field 0 at bit 0; bm: of their high parts)
     uint32_t b0, b1, b2;      // field widths
     uint32_t f0, f1, f2;      // field masks
     uint32_t low2;            // in-brick bits of every field, 4^3 bricks
     uint32_t kmul, kshr;      // in-brick cell index: ((pc & low2) * kmul) >> kshr = x | y << 2 | z << 4
+    uint32_t bm;              // brick-major layout (then low2 = 63, kmul = 1, kshr = 0)
 };
 constexpr uint32_t kPackMaxRes = 1024;                         // cells per axis a packed walk holds
 ZHD uint32_t ceil_log2u(uint32_t x) {
@@ -243,7 +253,30 @@ ZHD uint32_t div_by(uint32_t n, const DivS& d) { return (uint32_t)(((uint64_t)n 
 // linear index on power-of-two grids), widened where close fields would make
 // the in-brick multiplier's bit pairs overlap (small grids; they then index a
 // padded copy of the cells).
-ZHD bool pack_layout(const uint32_t res[3], PackK& k) {
+// The brick-major layout, if the grid allows it.
+ZHD bool pack_layout_bm(const uint32_t res[3], PackK& k) {
+    uint32_t bb[3];
+    for (int a = 0; a < 3; ++a) {
+        if (res[a] < 4u || res[a] > kPackMaxRes || (res[a] & (res[a] - 1u)) != 0u) return false;
+        bb[a] = ceil_log2u(res[a]);
+    }
+    if (bb[0] + bb[1] + bb[2] > 30u) return false;
+    k.b0 = bb[0]; k.b1 = bb[1]; k.b2 = bb[2];
+    k.o1 = 6u + (bb[0] - 2u);
+    k.o2 = k.o1 + (bb[1] - 2u);
+    k.f0 = 3u | (((1u << (bb[0] - 2u)) - 1u) << 6u);
+    k.f1 = (3u << 2u) | (((1u << (bb[1] - 2u)) - 1u) << k.o1);
+    k.f2 = (3u << 4u) | (((1u << (bb[2] - 2u)) - 1u) << k.o2);
+    k.low2 = 63u;
+    k.kmul = 1u;
+    k.kshr = 0u;
+    k.bm = 1u;
+    return true;
+}
+// BM_OK: the brick-major layout where the grid allows it (pack_layout_bm).
+ZHD bool pack_layout(const uint32_t res[3], PackK& k, bool bm_ok = false) {
+    if (bm_ok && pack_layout_bm(res, k)) return true;
+    k.bm = 0u;
     uint32_t b[3];
     for (int a = 0; a < 3; ++a) {
         if (res[a] == 0 || res[a] > kPackMaxRes) return false;
@@ -254,27 +287,64 @@ ZHD bool pack_layout(const uint32_t res[3], PackK& k) {
             if (pack_fields(b[0] + e0, b[1] + (extra - e0), b[2], k)) return true;
     return false;
 }
-ZHD uint32_t pack_cellv(const PackK& k, uint32_t c0, uint32_t c1, uint32_t c2) {
+template <bool BM>
+ZHD uint32_t pack_cellt(const PackK& k, uint32_t c0, uint32_t c1, uint32_t c2) {
+    if (BM)
+        return (c0 & 3u) | ((c1 & 3u) << 2) | ((c2 & 3u) << 4) | ((c0 >> 2) << 6) | ((c1 >> 2) << k.o1) |
+               ((c2 >> 2) << k.o2);
     return c0 | (c1 << k.o1) | (c2 << k.o2);
+}
+ZHD uint32_t pack_cellv(const PackK& k, uint32_t c0, uint32_t c1, uint32_t c2) {
+    return k.bm ? pack_cellt<true>(k, c0, c1, c2) : pack_cellt<false>(k, c0, c1, c2);
 }
 // whether the packed word equals the linear cell index (no padded copy needed)
 ZHD bool pack_is_linear(const uint32_t res[3], const PackK& k) {
-    return res[0] == (1u << k.b0) && res[1] == (1u << k.b1) && res[2] == (1u << k.b2);
+    return !k.bm && res[0] == (1u << k.b0) && res[1] == (1u << k.b1) && res[2] == (1u << k.b2);
+}
+// Axis a's cell coordinate of a packed word
+ZHD uint32_t pack_coord(const PackK& k, uint32_t pc, int a) {
+    const uint32_t o = a == 0 ? 0u : (a == 1 ? k.o1 : k.o2), b = a == 0 ? k.b0 : (a == 1 ? k.b1 : k.b2);
+    if (k.bm) return ((pc >> (2 * a)) & 3u) | (((pc >> (a == 0 ? 6u : o)) & ((1u << (b - 2u)) - 1u)) << 2);
+    return (pc >> o) & (b >= 32u ? ~0u : (1u << b) - 1u);
+}
+// pc + D on field F (D = +-lowbit(F), one cell): one add for contiguous
+// fields; for brick-major ones the gap between the field's two runs is filled
+// with ones (forward: the carry crosses it) or cleared (backward: the borrow
+// does), the sum masked to F and the other fields kept.  No carry leaves the
+// field.  (pk_addn: n cells.)
+template <bool BM>
+ZHD uint32_t pk_add(uint32_t pc, uint32_t f, uint32_t d) {
+    if (!BM) return pc + d;
+    const uint32_t s = (uint32_t)((int32_t)d >> 31);
+    const uint32_t g = (pc & f) | (~f & ~s);
+    return ((g + d) & f) | (pc & ~f);
+}
+template <bool BM>
+ZHD uint32_t pk_addn(uint32_t pc, uint32_t f, uint32_t n, uint32_t d) {
+    if (!BM) return pc + n * d;
+    for (uint32_t i = 0; i < n; ++i) pc = pk_add<true>(pc, f, d);
+    return pc;
 }
 struct DdaV {
     float tn0, tn1, tn2, td0, td1, td2;
     uint32_t pc, pe;
     uint32_t d0, d1, d2;      // packed cell step per axis
 };
-ZHD void ddav_from(const Dda& d, const GridK& g, const PackK& k, DdaV& w) {
+template <bool BM>
+ZHD void ddav_from_t(const Dda& d, const GridK& g, const PackK& k, DdaV& w) {
     w.tn0 = d.tn0; w.tn1 = d.tn1; w.tn2 = d.tn2;
     w.td0 = d.td0; w.td1 = d.td1; w.td2 = d.td2;
-    w.pc = pack_cellv(k, d.c0, d.c1, d.c2);
+    w.pc = pack_cellt<BM>(k, d.c0, d.c1, d.c2);
     const bool n0 = d.neg & 1u, n1 = (d.neg >> 1) & 1u, n2 = (d.neg >> 2) & 1u;
-    w.pe = pack_cellv(k, n0 ? 0u : g.rm0, n1 ? 0u : g.rm1, n2 ? 0u : g.rm2);
+    w.pe = pack_cellt<BM>(k, n0 ? 0u : g.rm0, n1 ? 0u : g.rm1, n2 ? 0u : g.rm2);
+    const uint32_t s1 = BM ? 4u : (1u << k.o1), s2 = BM ? 16u : (1u << k.o2);
     w.d0 = n0 ? 0xFFFFFFFFu : 1u;
-    w.d1 = n1 ? 0u - (1u << k.o1) : (1u << k.o1);
-    w.d2 = n2 ? 0u - (1u << k.o2) : (1u << k.o2);
+    w.d1 = n1 ? 0u - s1 : s1;
+    w.d2 = n2 ? 0u - s2 : s2;
+}
+ZHD void ddav_from(const Dda& d, const GridK& g, const PackK& k, DdaV& w) {
+    if (k.bm) ddav_from_t<true>(d, g, k, w);
+    else ddav_from_t<false>(d, g, k, w);
 }
 // An opaque copy: keeps the compiler from merging `a0 ? t2 : (a1 ? t2 : u)`
 // into `(a0 || a1) ? t2 : u`, whose or-of-compares it turns into a select of
@@ -300,7 +370,7 @@ ZHD float opaque_f(float x) {
         const float tc_ = a0_ ? t0_ : (a1_ ? t1_ : t2_);                             \
         const float dt_ = a0_ ? (S).td0 : (a1_ ? (S).td1 : (S).td2);                 \
         const uint32_t fm_ = a0_ ? (K).f0 : (a1_ ? (K).f1 : (K).f2);                 \
-        const uint32_t pn_ = (S).pc + (a0_ ? (S).d0 : (a1_ ? (S).d1 : (S).d2));      \
+        const uint32_t pn_ = pk_add<PK_BM>((S).pc, fm_, a0_ ? (S).d0 : (a1_ ? (S).d1 : (S).d2)); \
         (CROSSED) = (((S).pc ^ pn_) & ~(LOWM)) != 0u;                                \
         (EXITED) = (((S).pc ^ (S).pe) & fm_) == 0u;                                  \
         (TC) = tc_;                                                                  \
@@ -368,13 +438,13 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
     do {                                                                             \
         DDAV_STEPM_CORE(S, FV0, FV1, FV2, fm_, dp_, TC)                              \
         (EXM) = lm_of((((S).pc ^ (S).pe) & fm_) == 0u);                              \
-        (S).pc += dp_;                                                               \
+        (S).pc = pk_add<PK_BM>((S).pc, fm_, dp_);                                           \
     } while (0)
 // The same with DDAV_STEPX's per-lane outputs (the lane walk)
 #define DDAV_STEPMB(S, FV0, FV1, FV2, LOWM, CROSSED, EXITED, TC)                     \
     do {                                                                             \
         DDAV_STEPM_CORE(S, FV0, FV1, FV2, fm_, dp_, TC)                              \
-        const uint32_t pn_ = (S).pc + dp_;                                           \
+        const uint32_t pn_ = pk_add<PK_BM>((S).pc, fm_, dp_);                               \
         (CROSSED) = (((S).pc ^ pn_) & ~(LOWM)) != 0u;                                \
         (EXITED) = (((S).pc ^ (S).pe) & fm_) == 0u;                                  \
         (S).pc = pn_;                                                                \
@@ -459,11 +529,11 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
 #else
 #define ZRT_UBFE(X, O, W) ((W) == 0u ? 0u : (((X) >> (O)) & (0xFFFFFFFFu >> (32u - (W)))))
 #endif
-#define SKIPV_AXIS(S, A, OA, BA)                                                               \
-    const uint32_t c##A##_ = ZRT_UBFE((S).pc, (OA), (BA));                                      \
+#define SKIPV_AXIS(S, K, A)                                                                    \
+    const uint32_t c##A##_ = pack_coord((K), (S).pc, A);                                        \
     const uint32_t xn##A##_ = (uint32_t)((int32_t)(S).d##A >> 31);                              \
     const uint32_t rem##A##_ = ~(c##A##_ ^ xn##A##_) & 3u;                                      \
-    const uint32_t te##A##_ = xn##A##_ ? c##A##_ : ZRT_UBFE((S).pe, (OA), (BA)) - c##A##_;      \
+    const uint32_t te##A##_ = xn##A##_ ? c##A##_ : pack_coord((K), (S).pe, A) - c##A##_;        \
     const uint32_t m1##A##_ = zmin(rem##A##_, te##A##_);                                        \
     const bool out##A##_ = te##A##_ <= rem##A##_;                                               \
     const float T##A##1_ = (S).tn##A;                                                           \
@@ -482,9 +552,9 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
               : (k##A##_ == 2u ? T##A##3_ : (k##A##_ == 3u ? T##A##4_ : T##A##4_ + (S).td##A)));
 #define BRICK_SKIPV(S, K, EXITED, TC)                                                          \
     do {                                                                                       \
-        SKIPV_AXIS(S, 0, 0u, (K).b0)                                                           \
-        SKIPV_AXIS(S, 1, (K).o1, (K).b1)                                                       \
-        SKIPV_AXIS(S, 2, (K).o2, (K).b2)                                                       \
+        SKIPV_AXIS(S, K, 0)                                                                    \
+        SKIPV_AXIS(S, K, 1)                                                                    \
+        SKIPV_AXIS(S, K, 2)                                                                    \
         const bool x0_ = E0_ < E1_ && E0_ < E2_;                                               \
         const bool x1_ = !(E0_ < E1_) && E1_ < E2_;                                            \
         const bool x2_ = !x0_ && !x1_;                                                         \
@@ -494,7 +564,8 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
         SKIPV_COUNT(S, 2, !x2_)                                                                \
         (EXITED) = x0_ ? out0_ : (x1_ ? out1_ : out2_);                                        \
         (TC) = ex_;                                                                            \
-        (S).pc += k0_ * (S).d0 + k1_ * (S).d1 + k2_ * (S).d2;                                  \
+        (S).pc = pk_addn<PK_BM>(pk_addn<PK_BM>(pk_addn<PK_BM>((S).pc, (K).f0, k0_, (S).d0), (K).f1, k1_, (S).d1), (K).f2, \
+                         k2_, (S).d2);                                                         \
     } while (0)
 
 // Fast-forward of the packed walk through space known to be empty: every
@@ -512,7 +583,7 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
     while ((S).tn##A < (TAU)) {                                                                \
         if ((((S).pc ^ (S).pe) & (FA)) == 0u) { (EXITED) = true; break; }                     \
         (S).tn##A += (S).td##A;                                                                \
-        (S).pc += (S).d##A;                                                                    \
+        (S).pc = pk_add<PK_BM>((S).pc, (FA), (S).d##A);                                               \
     }
 #define DDAV_FF(S, F0, F1, F2, TAU, EXITED)                                                    \
     do {                                                                                       \
@@ -533,7 +604,7 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
             (EXITED) = (EXITED) || (go_ && at_);                                               \
             const bool mv_ = go_ && !at_;                                                      \
             (S).tn##A = mv_ ? (S).tn##A + (S).td##A : (S).tn##A;                               \
-            (S).pc = mv_ ? (S).pc + (S).d##A : (S).pc;                                         \
+            (S).pc = mv_ ? pk_add<PK_BM>((S).pc, (FA), (S).d##A) : (S).pc;                           \
         }                                                                                      \
         if (!((S).tn##A < (TAU)) || (EXITED)) break;                                           \
     }
@@ -551,25 +622,25 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
 // same adds in the same order: the state is the one the cell walk reaches
 // after them) and one packed-cell step of n cells, then FF_AXIS for the last
 // few.  Same crossings, same state, same EXITED as DDAV_FF.
-#define FFC_AXIS(S, A, FA, OA, BA, TAU, EXITED)                                                \
+#define FFC_AXIS(S, K, A, FA, TAU, EXITED)                                                     \
     {                                                                                          \
         const float est_ = ((TAU) - (S).tn##A) / (S).td##A;                                    \
         /* a lower bound on the crossings below TAU: the n adds' rounding drifts by at most */ \
         /* n TAU 2^-24 <= 6e-5 n td while TAU < 1000 td, inside the 1e-4 n + 2 margin     */ \
         uint32_t n_ = est_ > 3.0f && (TAU) < 1000.0f * (S).td##A ? (uint32_t)(est_ * 0.9999f) - 2u : 0u; \
-        const uint32_t c_ = ZRT_UBFE((S).pc, (OA), (BA)), e_ = ZRT_UBFE((S).pe, (OA), (BA));  \
+        const uint32_t c_ = pack_coord((K), (S).pc, A), e_ = pack_coord((K), (S).pe, A);      \
         const uint32_t left_ = c_ > e_ ? c_ - e_ : e_ - c_;   /* cells before the exit one */  \
         n_ = zmin(n_, left_);                                                                  \
         for (uint32_t k_ = 0; k_ < n_; ++k_) (S).tn##A += (S).td##A;                           \
-        (S).pc += n_ * (S).d##A;                                                               \
+        (S).pc = pk_addn<PK_BM>((S).pc, (FA), n_, (S).d##A);                                          \
     }                                                                                          \
     FF_AXIS(S, A, FA, TAU, EXITED)
 #define DDAV_FFC(S, K, F0, F1, F2, TAU, EXITED)                                                \
     do {                                                                                       \
         (EXITED) = false;                                                                      \
-        FFC_AXIS(S, 0, F0, 0u, (K).b0, TAU, EXITED)                                            \
-        if (!(EXITED)) { FFC_AXIS(S, 1, F1, (K).o1, (K).b1, TAU, EXITED) }                     \
-        if (!(EXITED)) { FFC_AXIS(S, 2, F2, (K).o2, (K).b2, TAU, EXITED) }                     \
+        FFC_AXIS(S, K, 0, F0, TAU, EXITED)                                                     \
+        if (!(EXITED)) { FFC_AXIS(S, K, 1, F1, TAU, EXITED) }                                  \
+        if (!(EXITED)) { FFC_AXIS(S, K, 2, F2, TAU, EXITED) }                                  \
     } while (0)
 
 // Select of the park kernel's pair refill (render.hip): position of the r-th

@@ -111,6 +111,13 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #define ZRT_FRUSTUM_SHIFT 3
 #endif
 constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
+// brick-major packed cell words for the grids that allow them (dda.h): r05ag,
+// 2 rounds, images identical: cfg3 6076 / 6088 vs 6005 / 5999 (+1.3%), cfg2
+// +2.4%, cfg5 +1.2%; the park walk trip 179 -> 165 VALU
+// (profiles/r05/r05ag_ab_brick_major.log)
+#ifndef ZRT_PACK_BM
+#define ZRT_PACK_BM 1
+#endif
 constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
@@ -200,7 +207,14 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
 
 // brick_occupied for a packed cell (DdaV): the brick coordinates are bit
 // fields of the word (width 0 when a brick spans the whole axis)
+// (brick-major words: the occupancy bricks are 4^3, context_packed, so the
+// brick is the word's high part)
+template <bool BM>
 __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uint32_t* occ, uint32_t pc) {
+    if (BM) {
+        const uint32_t b = pc >> 6;
+        return (occ[b >> 5] >> (b & 31u)) & 1u;
+    }
     const uint32_t b = __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o2, p.occ_w2), p.occ_nb01) +
                        __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
                        __builtin_amdgcn_ubfe(pc, p.occ_shift, p.occ_w0);
@@ -212,7 +226,9 @@ __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uin
 // (pack_layout picks the multiplier and checks every in-brick cell), and the
 // 64-bit shift reads only k[5:0].  (6 VALU; 9 with the fields moved by shifts
 // and masks.)
+template <bool BM>
 __device__ __forceinline__ bool occx_cell(unsigned long long bm, const DdaV& s, const PackK& k) {
+    if (BM) return (uint32_t)(bm >> (s.pc & 63u)) & 1u;   // (brick-major: the word's low six bits)
     const uint32_t i = __umul24(s.pc & k.low2, k.kmul) >> k.kshr;
     return (uint32_t)(bm >> (i & 63u)) & 1u;
 }
@@ -271,7 +287,7 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // TAU (packed walk): a frustum bound (escape.h frustum_bound lo) for this ray: the
 // crossings below it enter only empty cells; +inf: the ray meets no
 // occupied cell at all.
-template <bool STATS, int TB, bool PACKED = false>
+template <bool STATS, int TB, bool PACKED = false, bool PK_BM = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr,
@@ -284,7 +300,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
     if constexpr (PACKED) {
         static_assert(!STATS, "the counting build walks unpacked");
         DdaV s;
-        ddav_from(s0, gk, p.pk, s);
+        ddav_from_t<PK_BM>(s0, gk, p.pk, s);
         // the field masks as laundered registers: selected straight from the
         // kernel arguments they became a vector load at a selected offset
         // (v_cndmask of 0x94/0x98/0x9c, global_load_dword, vmcnt(0)) in
@@ -304,7 +320,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                 if (exited) return nearest;
             }
         }
-        bool occupied = brick_occupied_v(p, occ, s.pc);
+        bool occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
         // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
         // bound) the t past which every cell of the ray is empty
         float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
@@ -320,7 +336,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
             DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
-            if (crossed) occupied = brick_occupied_v(p, occ, s.pc);
+            if (crossed) occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
         }
         return nearest;
     }
@@ -775,7 +791,7 @@ __device__ __forceinline__ void path_state(const WfParams& w, uint32_t i, uint32
 }
 
 // wf_kernel: one lane = one segment, walked and tested by the lane itself.
-template <int MINW, bool PRIMARY, bool PACKED>
+template <int MINW, bool PRIMARY, bool PACKED, bool PK_BM = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -837,7 +853,7 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             uint32_t hidx = 0;
             WF_STAMP(2);
             if (depth != 0)
-                t = trace_ray<false, kTriBatch, PACKED>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
+                t = trace_ray<false, kTriBatch, PACKED, PK_BM>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
                                                         tau, tfar);
             WF_STAMP(0);
             uint32_t item, slot;
@@ -928,7 +944,9 @@ __device__ __forceinline__ unsigned long long occx_mask_clamped(const OccX& L, u
 // bits above their low two.  24-bit multiplies (full rate; v_mul_lo_u32 is
 // quarter rate), exact because OccX serves only grids of at most 2^24
 // bricks (occx_usable).
+template <bool BM>
 __device__ __forceinline__ uint32_t occx_brick(const WfParams& w, const DdaV& s) {
+    if (BM) return s.pc >> 6;                              // (brick-major: the brick's linear index)
     const TraceParams& p = w.t;
     return __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox2, p.ow2), w.occx_nb01) +
            __umul24(__builtin_amdgcn_ubfe(s.pc, p.ox1, p.ow1), w.occx_nb0) + __builtin_amdgcn_ubfe(s.pc, 2u, p.ow0);
@@ -1080,8 +1098,9 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 #else
 #define ZRT_PARK_ATTR
 #endif
-// ESC: with the escape table (context_escape decides per scene)
-template <bool ESC>
+// ESC: with the escape table (context_escape decides per scene); PK_BM:
+// brick-major packed words (dda.h)
+template <bool ESC, bool PK_BM>
 __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -1194,7 +1213,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                             W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
                             Dda s0;
                             if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
-                                ddav_from(s0, gk, pk, s);
+                                ddav_from_t<PK_BM>(s0, gk, pk, s);
                                 if (ESC) {
                                     // (every DMA into this slot from the lane's last
                                     // ray has landed: its kDone drained vmcnt above)
@@ -1204,7 +1223,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                                     eb = ~0u;
                                     esc_slot[lane] = 0u;
                                 }
-                                if (occx_cell(occx_mask(L, occx_brick(w, s)), s, pk)) {
+                                if (occx_cell<PK_BM>(occx_mask(L, occx_brick<PK_BM>(w, s)), s, pk)) {
                                     park_load_range(p, s.pc, rng_slot);
                                     rng_slot[128 + lane] = ~0u;    // first cell: every ref
                                     st = kPark;
@@ -1262,13 +1281,13 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                     DDAV_STEPM(ss[k], fv0, fv1, fv2, ex[k], te[k]);
                 }
 #pragma unroll
-                for (int k = 0; k < kS; ++k) q[k] = occx_mask_clamped(L, occx_brick(w, ss[k]), w.occx_nbw);
+                for (int k = 0; k < kS; ++k) q[k] = occx_mask_clamped(L, occx_brick<PK_BM>(w, ss[k]), w.occx_nbw);
 #pragma unroll
                 for (int k = 0; k < kS; ++k) asm volatile("" : "+v"(q[k]));
 #pragma unroll
                 for (int k = 0; k < kS; ++k) {
                     dd[k] = lm_or(ex[k], lm_of(nearest <= te[k]));
-                    stop[k] = lm_or(dd[k], lm_of(occx_cell(q[k], ss[k], pk)));
+                    stop[k] = lm_or(dd[k], lm_of(occx_cell<PK_BM>(q[k], ss[k], pk)));
                 }
                 // the first stopping step wins: from the last step back (the
                 // last step's selects are identities)
@@ -1320,7 +1339,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                     st = lm_selu(esc, kDone, st);
                     // one query per brick the ray enters (its word does not
                     // change while the lane walks inside the brick)
-                    const uint32_t b = occx_brick(w, s);
+                    const uint32_t b = occx_brick<PK_BM>(w, s);
                     if (st == kWalk && emask != 0u && b != eb) {
                         park_load_esc(reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(w.esc) +
                                                                         b * (4u * kEscWords) + eoff),
@@ -1721,6 +1740,8 @@ constexpr uint32_t kParkRefillMin = ZRT_PARK_R;
 // packed walk state when every axis has at most kPackMaxRes cells
 const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true, true>;
 const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false, true>;
+const WfFn kWfPrimaryBM = (WfFn)wf_kernel<kWfMinWaves0, true, true, true>;
+const WfFn kWfBounceBM = (WfFn)wf_kernel<kWfMinWaves, false, true, true>;
 const WfFn kWfPrimaryWide = (WfFn)wf_kernel<kWfMinWaves0, true, false>;
 const WfFn kWfBounceWide = (WfFn)wf_kernel<kWfMinWaves, false, false>;
 
@@ -1896,8 +1917,11 @@ extern "C" const char* zrt_timed_kernels(void) {
     // the default launch set: primary wf_kernel, then per bounce the
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
-    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1EE,wf_park_kernelILb1E,wf_park_kernelILb0E,wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(
-        ZRT_WF_MINW) "ELb0ELb1EE";
+    // (brick-major packed words, then field words: dda.h)
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb1EE,wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb0EE,"
+           "wf_park_kernelILb1ELb1E,wf_park_kernelILb0ELb1E,wf_park_kernelILb1ELb0E,wf_park_kernelILb0ELb0E,"
+           "wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(ZRT_WF_MINW) "ELb0ELb1ELb1EE,wf_kernelILi" ZRT_STR(
+               ZRT_WF_MINW) "ELb0ELb1ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
@@ -2044,12 +2068,12 @@ __device__ __forceinline__ bool same_tri(const float* pos, uint32_t a, uint32_t 
 // the contest stand-in repeat the previous cell's (triangles span ~5.6
 // cells), a third on the Sponza-scale one.
 __global__ __launch_bounds__(kBlock) void cell32_kernel(const uint2* __restrict__ cells, uint32_t r0, uint32_t r1,
-                                                        uint32_t r2, uint32_t ncells, uint32_t o1, uint32_t o2,
+                                                        uint32_t r2, uint32_t ncells, const PackK pk,
                                                         const float* __restrict__ pos, uint32_t* __restrict__ out) {
     for (uint32_t ci = blockIdx.x * kBlock + threadIdx.x; ci < ncells; ci += gridDim.x * kBlock) {
         const uint2 c = cells[ci];
         const uint32_t x = ci % r0, y = (ci / r0) % r1, z = ci / r0 / r1;
-        uint32_t* rec = out + 8ull * (x | (y << o1) | (z << o2));
+        uint32_t* rec = out + 8ull * pack_cellv(pk, x, y, z);
         rec[0] = c.x;
         rec[1] = c.y;
         const uint32_t n = c.y - c.x;
@@ -2081,7 +2105,9 @@ __global__ __launch_bounds__(kBlock) void cell32_kernel(const uint2* __restrict_
 constexpr uint64_t kCell32Max = 16ull << 30;
 static int context_packed(zrt_context* c) {
     const uint32_t* r = c->grid.resolution;
-    c->packed = pack_layout(r, c->pk);
+    // brick-major words where the grid allows them and the primary's
+    // occupancy bricks are 4^3 (it reads them by pc >> 6); else field words
+    c->packed = pack_layout(r, c->pk, ZRT_PACK_BM && c->occ_shift == 2u);
     if (!c->packed) return ZRT_OK;
     const uint64_t n = 1ull << (c->pk.b0 + c->pk.b1 + c->pk.b2);
     if (32 * n > kCell32Max || (n > 16ull * c->ncells && 32 * n > (1ull << 30))) {
@@ -2091,7 +2117,7 @@ static int context_packed(zrt_context* c) {
     HIP_TRY(hipMalloc((void**)&c->d_cell32, 32 * n));
     if (!pack_is_linear(r, c->pk)) HIP_TRY(hipMemsetAsync(c->d_cell32, 0, 32 * n, c->stream));
     hipLaunchKernelGGL(cell32_kernel, dim3(std::min<uint32_t>((c->ncells + kBlock - 1) / kBlock, 16384)), dim3(kBlock),
-                       0, c->stream, c->d_cells, r[0], r[1], r[2], c->ncells, c->pk.o1, c->pk.o2, c->d_pos,
+                       0, c->stream, c->d_cells, r[0], r[1], r[2], c->ncells, c->pk, c->d_pos,
                        c->d_cell32);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2777,7 +2803,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     const bool packed = c->packed;
-    const WfFn f_first = packed ? kWfPrimary : kWfPrimaryWide;
+    const bool pbm = packed && c->pk.bm;   // brick-major packed words (dda.h)
+    const WfFn f_first = packed ? (pbm ? kWfPrimaryBM : kWfPrimary) : kWfPrimaryWide;
     // the escape table: where dense enough to pay (context_escape), or as
     // the flags force it (both kernels give the same image)
     // (built at the first frame of 2^23 samples or more, or the first the flag
@@ -2789,8 +2816,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     }
     const bool esc = c->d_esc && !(cfg->flags & ZRT_FLAG_NO_ESCAPE) &&
                      (c->esc_on || (cfg->flags & ZRT_FLAG_ESCAPE));
-    const WfFn f_next = park_next ? (esc ? (WfFn)wf_park_kernel<true> : (WfFn)wf_park_kernel<false>)
-                                  : (packed ? kWfBounce : kWfBounceWide);
+    const WfFn f_next = park_next ? (pbm ? (esc ? (WfFn)wf_park_kernel<true, true> : (WfFn)wf_park_kernel<false, true>)
+                                         : (esc ? (WfFn)wf_park_kernel<true, false> : (WfFn)wf_park_kernel<false, false>))
+                                  : (packed ? (pbm ? kWfBounceBM : kWfBounce) : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
     const size_t lds_shade = c->nmat <= kLdsMats ? c->nmat * sizeof(DevMat) : 0;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
@@ -2878,13 +2906,14 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.cell32 = c->d_cell32;
     {
         const uint32_t sh = c->occ_shift, b[3] = {c->pk.b0, c->pk.b1, c->pk.b2};
-        auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
-        tp.occ_o1 = c->pk.o1 + sh;
-        tp.occ_o2 = c->pk.o2 + sh;
         tp.occ_w0 = b[0] > sh ? b[0] - sh : 0u;
         tp.occ_w1 = b[1] > sh ? b[1] - sh : 0u;
         tp.occ_w2 = b[2] > sh ? b[2] - sh : 0u;
-        tp.occ_lowm = lowbits(0) | (lowbits(1) << c->pk.o1) | (lowbits(2) << c->pk.o2);
+        auto lowbits = [&](int a) { return (1u << std::min(sh, b[a])) - 1u; };
+        tp.occ_o1 = c->pk.o1 + sh;
+        tp.occ_o2 = c->pk.o2 + sh;
+        // (brick-major words: occupancy bricks of 4^3, the word's low six bits)
+        tp.occ_lowm = c->pk.bm ? 63u : lowbits(0) | (lowbits(1) << c->pk.o1) | (lowbits(2) << c->pk.o2);
         tp.ox1 = c->pk.o1 + 2u;
         tp.ox2 = c->pk.o2 + 2u;
         tp.ow0 = b[0] - 2u;
