@@ -312,11 +312,22 @@ ZHD uint32_t pack_coord(const PackK& k, uint32_t pc, int a) {
 // with ones (forward: the carry crosses it) or cleared (backward: the borrow
 // does), the sum masked to F and the other fields kept.  No carry leaves the
 // field.  (pk_addn: n cells.)
+#ifndef ZRT_PK_BITOP3
+#define ZRT_PK_BITOP3 1
+#endif
 template <bool BM>
 ZHD uint32_t pk_add(uint32_t pc, uint32_t f, uint32_t d) {
     if (!BM) return pc + d;
     const uint32_t s = (uint32_t)((int32_t)d >> 31);
+#if defined(__HIP_DEVICE_COMPILE__) && ZRT_PK_BITOP3
+    // g = (pc & f) | (~f & ~s) as ONE v_bitop3 (table index pc*4 + f*2 + s:
+    // rows 0, 4, 6, 7 set); left to itself the compiler selects ~f by the
+    // sign with a compare, a select and a v_not (6 VALU per step, not 4)
+    uint32_t g;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd1" : "=v"(g) : "v"(pc), "v"(f), "v"(s));
+#else
     const uint32_t g = (pc & f) | (~f & ~s);
+#endif
     return ((g + d) & f) | (pc & ~f);
 }
 template <bool BM>
