@@ -118,6 +118,7 @@ constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
 #ifndef ZRT_PACK_BM
 #define ZRT_PACK_BM 1
 #endif
+
 constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
@@ -212,8 +213,7 @@ __device__ __forceinline__ bool brick_occupied(const TraceParams& p, const uint3
 template <bool BM>
 __device__ __forceinline__ bool brick_occupied_v(const TraceParams& p, const uint32_t* occ, uint32_t pc) {
     if (BM) {
-        const uint32_t b = pc >> 6;
-        return (occ[b >> 5] >> (b & 31u)) & 1u;
+        return __builtin_amdgcn_ubfe(occ[pc >> 11], pc >> 6, 1u);
     }
     const uint32_t b = __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o2, p.occ_w2), p.occ_nb01) +
                        __umul24(__builtin_amdgcn_ubfe(pc, p.occ_o1, p.occ_w1), p.occ_nb0) +
@@ -940,6 +940,13 @@ __device__ __forceinline__ unsigned long long occx_mask(const OccX& L, uint32_t 
 __device__ __forceinline__ unsigned long long occx_mask_clamped(const OccX& L, uint32_t b, uint32_t nbw) {
     return occx_mask_at(L, L.ent[min(b >> 5, nbw - 1u)], b);
 }
+// occx_mask for a brick-major word (no clamp: the word stays inside the
+// grid's packed range).  Laundering pc >> 11 saves the compiler's third
+// address VALU ((pc >> 8) & ~7 + base) but measured neutral (r05al:
+// cfg3 -0.2%, cfg2 / cfg5 +0.5%)
+__device__ __forceinline__ unsigned long long occx_mask_bm(const OccX& L, uint32_t pc) {
+    return occx_mask_at(L, L.ent[pc >> 11], pc >> 6);
+}
 // The 4^3 brick of a packed cell (DdaV): its coordinates are the fields'
 // bits above their low two.  24-bit multiplies (full rate; v_mul_lo_u32 is
 // quarter rate), exact because OccX serves only grids of at most 2^24
@@ -1281,7 +1288,11 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                     DDAV_STEPM(ss[k], fv0, fv1, fv2, ex[k], te[k]);
                 }
 #pragma unroll
-                for (int k = 0; k < kS; ++k) q[k] = occx_mask_clamped(L, occx_brick<PK_BM>(w, ss[k]), w.occx_nbw);
+                // (brick-major words never leave the grid's packed range, pk_add
+                // wraps inside a field, so their speculative lookups need no clamp)
+                for (int k = 0; k < kS; ++k)
+                    q[k] = PK_BM ? occx_mask_bm(L, ss[k].pc)
+                                 : occx_mask_clamped(L, occx_brick<PK_BM>(w, ss[k]), w.occx_nbw);
 #pragma unroll
                 for (int k = 0; k < kS; ++k) asm volatile("" : "+v"(q[k]));
 #pragma unroll
