@@ -208,6 +208,11 @@ typedef struct zrt_outputs {
     void* device_rgb_packed;         /* device n_owned*3 on the context's device */
 } zrt_outputs;
 
+/* Both creators return ZRT_ERR_UNSUPPORTED for a triangle edge component
+ * (scene->triangles_pos e1, e2) of magnitude 2^62 or more, or a vertex
+ * component (positions) of 2^61 or more: the kernels' exact reciprocal of the
+ * Moller-Trumbore determinant holds for |det| < 2^126.  NaN components are
+ * taken and never hit, as in the reference. */
 int zrt_context_create(const zrt_scene* scene, int device, zrt_context** out);
 /* Geometry.build + bakeInto (stage2.zig:44-164, main.zig:117-118) and the
  * stage-3 upload in one step: the grid is built on `device` straight into the

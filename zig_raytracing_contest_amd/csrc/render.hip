@@ -1888,6 +1888,10 @@ static int validate_scene(const zrt_scene* s) {
     }
     for (uint32_t i = 0; i < s->num_triangles; ++i)
         if (s->triangles_material[i] >= s->num_materials) return ZRT_ERR_INVALID_ARG;
+    // edge components below 2^62 (the kernels' exact reciprocal of the
+    // Moller-Trumbore determinant holds below 2^126: zrt_math.h mt_inv_det)
+    for (uint64_t k = 0; k < 9ull * s->num_triangles; ++k)
+        if (k % 9 >= 3 && fabsf(s->triangles_pos[k]) >= 0x1p62f) return ZRT_ERR_UNSUPPORTED;
     return validate_materials(s);
 }
 
@@ -2562,6 +2566,11 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
     if (rc != ZRT_OK) return rc;
     for (uint32_t i = 0; i < num_triangles; ++i)
         if (material[i] >= num_materials) return ZRT_ERR_INVALID_ARG;
+    // vertex components below 2^61, so every edge component is below 2^62
+    // (validate_scene)
+    if (num_triangles && !positions) return ZRT_ERR_INVALID_ARG;
+    for (uint64_t k = 0; k < 9ull * num_triangles; ++k)
+        if (fabsf(positions[k]) >= 0x1p61f) return ZRT_ERR_UNSUPPORTED;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
     if (device < 0) {

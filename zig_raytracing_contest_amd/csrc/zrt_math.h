@@ -292,11 +292,33 @@ ZHD double rng_norm64(Rng& r, const double* zx, const double* zf) {
 }
 
 // ---- Moller-Trumbore, back faces culled (linalg.zig:696-722) --------------
+#ifndef ZRT_MT_RCP
+#define ZRT_MT_RCP 1
+#endif
+// 1.0f / det, correctly rounded.  On the device: the compiler's IEEE f32
+// division sequence (rcp, then the fma refinements) without its
+// v_div_scale / v_div_fmas / v_div_fixup steps, which are identities for a
+// numerator of 1 and 2^-95 < |det| < 2^126 (no scaling, no special value):
+// 7 VALU instead of 11 (r05am).  A det below 1e-8 is rejected whatever this
+// returns, and |det| <= |e1| |e2| < 2^126 because the contexts take no
+// triangle with an edge component of 2^62 or more (validate_scene, NaN
+// aside, which both forms propagate).  A guard per wave instead split the
+// test loop and spilled.
+ZHD float mt_inv_det(float det) {
+#if defined(__HIP_DEVICE_COMPILE__) && ZRT_MT_RCP
+    const float r = __builtin_amdgcn_rcpf(det);
+    const float f1 = __builtin_fmaf(__builtin_fmaf(-det, r, 1.0f), r, r);
+    const float f3 = __builtin_fmaf(__builtin_fmaf(-det, f1, 1.0f), f1, f1);
+    return __builtin_fmaf(__builtin_fmaf(-det, f3, 1.0f), f1, f3);
+#else
+    return 1.0f / det;
+#endif
+}
 ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
     if (det < 0.00000001f) return false;
-    const float inv_det = 1.0f / det;
+    const float inv_det = mt_inv_det(det);
     const v3 tvec = sub(o, v0);
     const float u = dot(tvec, pvec) * inv_det;
     if (u < 0.0f || u > 1.0f) return false;
@@ -318,7 +340,7 @@ ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv
 ZHD bool tri_ray_flat(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
-    const float inv_det = 1.0f / det;
+    const float inv_det = mt_inv_det(det);
     const v3 tvec = sub(o, v0);
     const float u = dot(tvec, pvec) * inv_det;
     const v3 qvec = cross(tvec, e1);
