@@ -674,7 +674,9 @@ ZHD uint32_t select_bit(const uint8_t* sel8, uint32_t m, uint32_t r) {
     const uint32_t c0 = (uint32_t)__builtin_popcount(m & 0xFFu), c1 = (uint32_t)__builtin_popcount(m & 0xFFFFu),
                    c2 = (uint32_t)__builtin_popcount(m & 0xFFFFFFu);
     const uint32_t k = (r >= c0 ? 1u : 0u) + (r >= c1 ? 1u : 0u) + (r >= c2 ? 1u : 0u);
-    const uint32_t below = k == 0u ? 0u : (k == 1u ? c0 : (k == 2u ? c1 : c2));
+    // (the bits below byte k counted again rather than picked from c0..c2:
+    // the pick compiled to three nested exec-mask branches, r05aq ISA)
+    const uint32_t below = (uint32_t)__builtin_popcount(m & ((1u << (8u * k)) - 1u));
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t byte = __builtin_amdgcn_ubfe(m, 8u * k, 8u);
 #else

@@ -1728,9 +1728,12 @@ using WfFn = void (*)(const WfParams);
 #endif
 // r04pw (the frustum-bound primary): 6 / 7 / 8 waves cfg3 5732 / 5724 / 5692,
 // cfg5 3491 / 3489 / 3493, cfg2 3778 / 3739 / 3725 Mrays/s; at 6 the primary
-// has no scratch access at all (12 at 7, 26 and walk reloads at 8)
+// has no scratch access at all (12 at 7, 26 and walk reloads at 8).  Built
+// without SLP pairing (Makefile) the packed primary fits 7 waves (72 VGPRs,
+// no spill): r05ap, cfg3 6412 / 6400 vs 6346 / 6357 (+0.9%), cfg2 +0.7%,
+// cfg5 +0.3% (profiles/r05/r05ap_ab_primary7_select.log)
 #ifndef ZRT_WF_MINW0
-#define ZRT_WF_MINW0 6
+#define ZRT_WF_MINW0 7
 #endif
 constexpr int kWfMinWaves = ZRT_WF_MINW;
 constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
@@ -1753,7 +1756,7 @@ const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true, true>;
 const WfFn kWfBounce = (WfFn)wf_kernel<kWfMinWaves, false, true>;
 const WfFn kWfPrimaryBM = (WfFn)wf_kernel<kWfMinWaves0, true, true, true>;
 const WfFn kWfBounceBM = (WfFn)wf_kernel<kWfMinWaves, false, true, true>;
-const WfFn kWfPrimaryWide = (WfFn)wf_kernel<kWfMinWaves0, true, false>;
+const WfFn kWfPrimaryWide = (WfFn)wf_kernel<kWfMinWaves, true, false>;   // (6 waves: at 7 it spills)
 const WfFn kWfBounceWide = (WfFn)wf_kernel<kWfMinWaves, false, false>;
 
 // max_bounce picks the stack depth the counting kernel is compiled for.
