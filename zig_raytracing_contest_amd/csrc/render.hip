@@ -1742,12 +1742,16 @@ constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
 // R 8/16/32; T 12 R 16 3110 Mrays/s, T 8-16 R 16 within 1.3%, R 8 -15%,
 // R 32 -13%; cfg5 T 16 R 16 2075, T 8 2055; full spp after the lane-mask
 // trip, r03z: T 14 vs 12 cfg3 +0.3%, cfg2 +0.6%, cfg5 +0.5%; T 10 / 16,
-// R 12 / 20 no better).  ZRT_SWEEP builds read ZRT_PARK_T / ZRT_PARK_R.
+// R 12 / 20 no better).  On round 5's final tree (cheaper walk trips and
+// test rounds) R 20 is ahead everywhere: r05au / r05av, 2 + 2 rounds, cfg3
+// +0.9 / +0.5%, cfg5 +0.25 / +0.3%, cfg2 +0.3 / +0.2%; T 12 / 16 / 18 and
+// R 12 / 24 are not (profiles/r05/r05au_ab_o2_park_schedule.log,
+// r05av_ab_park_schedule2.log).  ZRT_SWEEP builds read ZRT_PARK_T / ZRT_PARK_R.
 #ifndef ZRT_PARK_T
 #define ZRT_PARK_T 14
 #endif
 #ifndef ZRT_PARK_R
-#define ZRT_PARK_R 16
+#define ZRT_PARK_R 20
 #endif
 constexpr uint32_t kParkTestMin = ZRT_PARK_T;
 constexpr uint32_t kParkRefillMin = ZRT_PARK_R;
