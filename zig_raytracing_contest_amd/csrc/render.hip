@@ -69,10 +69,12 @@ constexpr int kParkBlock = ZRT_PARK_BLOCK_T;         // wf_park_kernel: one work
 #endif
 constexpr int kShadeEntries = ZRT_SHADE_N;           // wf_shade_kernel: queue entries per lane per fetch
 #ifndef ZRT_WF_CHUNK
-#define ZRT_WF_CHUNK 2
+#define ZRT_WF_CHUNK 3
 #endif
 // wf_kernel: 64-entry batches per work atomic (r02d1: 2 vs 1 cfg3 +0.35%,
-// cfg2 +0.9%, cfg5 +0.2%; 4: +0.6 / +0.5 / 0%)
+// cfg2 +0.9%, cfg5 +0.2%; 4: +0.6 / +0.5 / 0%; on round 5's final tree 3 vs
+// 2: cfg3 6548 / 6540 vs 6489 / 6499 (+0.8%), cfg2 +0.8%, cfg5 +0.1%,
+// profiles/r05/r05ay_ab_chunks_lead.log)
 constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 
 // Triangle positions per ref (bakeInto's Pos: v0, e1 = v1 - v0, e2 = v2 - v0)
