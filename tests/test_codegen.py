@@ -157,39 +157,74 @@ def test_park_walk_trip_is_not_a_register_shuffle(code):
         assert esc["execz"] <= plain["execz"] + 1, (bm, esc, plain)
 
 
+_WRITES01 = None
+
+
+def _s01_source(lines, k, loop=None):
+    """What s[0:1] holds at line k: 'spill' if the latest write to s0 or s1
+    before it in program order is a v_readlane_b32 (an SGPR spill reload),
+    'other' for any other write, 'entry' if nothing writes it first (the
+    kernel-argument pointer).  With loop = (b, e) holding k, a write to s0/s1
+    later in the loop body that is not a spill reload also makes it 'other'
+    (the back edge carries it to the use)."""
+    import re
+    w = re.compile(r"^\s*(\S+)\s+(s\[0:1\]|s0|s1)\s*,")
+    if loop is not None:
+        for j in range(k + 1, loop[1] + 1):
+            m = w.search(lines[j])
+            if m and m.group(1) != "v_readlane_b32":
+                return "other"
+    for j in range(k - 1, -1, -1):
+        m = w.search(lines[j])
+        if m:
+            return "spill" if m.group(1) == "v_readlane_b32" else "other"
+    return "entry"
+
+
 def test_walk_loops_load_nothing_from_the_kernel_arguments(code):
     """A select between kernel-argument fields (the packed walk's field masks
     f0/f1/f2) became, in round 3's primary lane walk, a vector load from the
     kernel-argument segment at a selected offset, waited on by a vmcnt(0) in
     every DDA step; the fields are laundered into registers now.  No timed
-    kernel may form a vector address from the kernel-argument pointer
-    (s[0:1] at entry) inside a loop -- unless the loop itself reloaded s0/s1
-    from an SGPR spill lane (v_readlane) before that use.  A scalar load into
-    s[0:1] does not count: it may reload the kernarg pointer itself (ADVICE
-    r4)."""
+    kernel may form a vector address from s[0:1] inside a loop unless the
+    latest write to s0/s1 before that use is an SGPR spill reload
+    (v_readlane, a spilled pointer such as the cell records' base): the
+    kernel-argument pointer itself (s[0:1] at entry, nothing written since)
+    and any other scalar write -- a scalar load may reload the kernarg
+    pointer -- are refused.  (Since r05ay the primary reloads
+    its cell-record base before the walk loop instead of in it.)"""
     import re
     sc, ks = code
-    writes01 = re.compile(r"^\s*v_readlane_b32\s+(s0|s1)\s*,")
+    use = re.compile(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]")
     for sub in sc.timed():
         ins = _kernel(ks, sub)
-        for b, e in _loops(ins):
-            body = [t.split("//")[0] for _, t in ins[b:e + 1]]
-            bad = [t.strip() for k, t in enumerate(body)
-                   if re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", t)
-                   and not any(writes01.search(x) for x in body[:k])]
-            assert not bad, (sub, bad[:2])
+        lines = [t.split("//")[0] for _, t in ins]
+        loops = _loops(ins)
+        for k in range(len(lines)):
+            if not use.search(lines[k]):
+                continue
+            inner = [(b, e) for b, e in loops if b <= k <= e]
+            if not inner:
+                continue
+            # (the innermost loop's back edge; an outer loop re-enters it
+            # through the code in front of its header, which the backward
+            # scan covers)
+            b, e = min(inner, key=lambda x: x[1] - x[0])
+            assert _s01_source(lines, k, (b, e)) == "spill", (sub, k, lines[k].strip())
 
 
 def test_kernel_argument_check_sees_a_kernarg_address():
-    """Control for the check above: a loop that forms an address from the
-    entry s[0:1] is caught, one that reloads s[0:1] first is not."""
-    import re
-    writes01 = re.compile(r"^\s*v_readlane_b32\s+(s0|s1)\s*,")
+    """Control for the check above: an address formed from the entry s[0:1]
+    or from s[0:1] written by a scalar load is caught; one after a spill
+    reload is not, nor is one whose loop rewrites s0/s1 only by reloads."""
     use = "v_lshl_add_u64 v[0:1], s[0:1], 0, v[0:1]"
-    assert not any(writes01.search(x) for x in ["v_add_f32 v1, v1, v2"])
-    assert writes01.search("v_readlane_b32 s0, v70, 31")
-    assert not writes01.search("s_load_dwordx2 s[0:1], s[4:5], 0x10")      # a kernarg reload is no exemption
-    assert re.search(r"v_lshl_add_u64 v\[\d+:\d+\], s\[0:1\]", use)
+    assert _s01_source(["v_add_f32 v1, v1, v2", use], 1) == "entry"
+    assert _s01_source(["v_readlane_b32 s0, v70, 31", "v_readlane_b32 s1, v70, 32", use], 2) == "spill"
+    assert _s01_source(["s_load_dwordx2 s[0:1], s[4:5], 0x10", use], 1) == "other"
+    assert _s01_source(["v_readlane_b32 s0, v70, 31", "v_readlane_b32 s1, v70, 32", use,
+                        "s_mov_b32 s0, 0x3ffffe"], 2, (0, 3)) == "other"
+    assert _s01_source(["v_readlane_b32 s0, v70, 31", "v_readlane_b32 s1, v70, 32", use,
+                        "v_readlane_b32 s0, v70, 31"], 2, (0, 3)) == "spill"
 
 
 def ins_after(ins, e, n=40):
