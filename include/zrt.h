@@ -134,6 +134,11 @@ typedef struct zrt_render_config {
                                         same image */
 #define ZRT_FLAG_NO_FRUSTUM   0x200u /* the primary launch never uses the frustum bounds (wins over
                                         ZRT_FLAG_FRUSTUM); same image */
+#define ZRT_FLAG_MT_EXACT     0x400u /* every launch walks + tests per lane with the IEEE f32 division in
+                                        Moller-Trumbore: what a context does by itself for a scene with
+                                        an edge component of 2^62 or more or infinite (the other kernels'
+                                        short reciprocal of the determinant holds for |det| < 2^126);
+                                        same image */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */
@@ -208,11 +213,13 @@ typedef struct zrt_outputs {
     void* device_rgb_packed;         /* device n_owned*3 on the context's device */
 } zrt_outputs;
 
-/* Both creators return ZRT_ERR_UNSUPPORTED for a triangle edge component
- * (scene->triangles_pos e1, e2) of magnitude 2^62 or more, or a vertex
- * component (positions) of 2^61 or more: the kernels' exact reciprocal of the
- * Moller-Trumbore determinant holds for |det| < 2^126.  NaN components are
- * taken and never hit, as in the reference. */
+/* Every finite, infinite or NaN coordinate is taken, as in the reference
+ * (linalg.zig:696-722).  A scene with a triangle edge component
+ * (scene->triangles_pos e1, e2) of magnitude 2^62 or more or infinite -- a
+ * vertex component (positions) of 2^61 or more for the device build --
+ * renders through the lane walk with the IEEE division (ZRT_FLAG_MT_EXACT),
+ * since the other kernels' short reciprocal of the Moller-Trumbore
+ * determinant is exact for |det| < 2^126 only. */
 int zrt_context_create(const zrt_scene* scene, int device, zrt_context** out);
 /* Geometry.build + bakeInto (stage2.zig:44-164, main.zig:117-118) and the
  * stage-3 upload in one step: the grid is built on `device` straight into the
@@ -318,6 +325,13 @@ enum {
     ZRT_PROBE_EXP_LOG = 6,    /* in n doubles -> out n*2 doubles (exp, log) */
     ZRT_PROBE_TEXTURE = 7,    /* in n*2 (u,v) + aux texture -> out n*3 */
     ZRT_PROBE_TRIANGLE_FLAT = 8, /* as TRIANGLE, through the branch-free test of the park kernel */
+    ZRT_PROBE_RECIP = 9,      /* in n floats det -> out n*2: the park / packed kernels' short 1/det
+                                 (rcp + six FMAs), the IEEE-division kernels' 1.0f/det */
+    ZRT_PROBE_RECIP_SWEEP = 10, /* in n*2 u32 {first float bits, count} -> out n*4 u32 {floats whose
+                                 short 1/det differs in any bit from the device's IEEE 1.0f/det (NaN
+                                 equals NaN), the smallest such bits (0xFFFFFFFF: none), 0, 0};
+                                 every float of each range, on the device */
+    ZRT_PROBE_TRIANGLE_EXACT = 11, /* as TRIANGLE, with the IEEE division of the ZRT_FLAG_MT_EXACT kernels */
 };
 int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device);
 /* Comma-separated substrings of the mangled names of the timed kernel

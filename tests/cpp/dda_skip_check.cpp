@@ -281,7 +281,7 @@ int main(int argc, char** argv) {
     const int n_rays = argc > 2 ? atoi(argv[2]) : 4000;
     std::mt19937_64 rng(12345);
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
-    uint64_t total = 0, skips = 0, ties = 0, fails = 0;
+    uint64_t total = 0, skips = 0, ties = 0, fails = 0, g_layout_grids = 0;
     for (int gi = 0; gi < n_grids; ++gi) {
         TestGrid g;
         const bool pow2 = gi % 3 == 0;     // exact arithmetic -> many crossing ties
@@ -297,6 +297,10 @@ int main(int argc, char** argv) {
         const float dens = (gi % 4) * 0.1f;
         for (auto& o : g.occ) o = U(rng) < dens;
         GridK k{g.res[0] - 1, g.res[1] - 1, g.res[2] - 1, g.res[0], g.res[0] * g.res[1]};
+        {   // grids whose packed words take this build's layout (the walk_skipv / walk_ff checks run on them)
+            PackK pk;
+            if (pack_layout(g.res, pk, PK_BM) && pk.bm == (uint32_t)PK_BM) ++g_layout_grids;
+        }
         for (int r = 0; r < n_rays; ++r) {
             v3 o, d;
             const int kind = r % 4;
@@ -338,10 +342,11 @@ int main(int argc, char** argv) {
     }
     fails += g_texit_fails + g_walk_fails + g_skipv_fails + g_ff_fails;
     printf("{\"rays\": %llu, \"skips\": %llu, \"tie_starts\": %llu, \"t_exit_fails\": %llu, "
-           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"skipv\": %llu, \"skipv_fails\": %llu, \"ff\": %llu, \"ff_steps\": %llu, \"ff_fails\": %llu, \"fails\": %llu}\n",
+           "\"walk_steps\": %llu, \"walk_fails\": %llu, \"skipv\": %llu, \"skipv_fails\": %llu, \"ff\": %llu, \"ff_steps\": %llu, \"ff_fails\": %llu, \"layout_grids\": %llu, \"fails\": %llu}\n",
            (unsigned long long)total, (unsigned long long)skips, (unsigned long long)ties,
            (unsigned long long)g_texit_fails, (unsigned long long)g_walk_steps, (unsigned long long)g_walk_fails,
            (unsigned long long)g_skipv, (unsigned long long)g_skipv_fails, (unsigned long long)g_ff,
-           (unsigned long long)g_ff_steps, (unsigned long long)g_ff_fails, (unsigned long long)fails);
+           (unsigned long long)g_ff_steps, (unsigned long long)g_ff_fails, (unsigned long long)g_layout_grids,
+           (unsigned long long)fails);
     return fails ? 1 : 0;
 }

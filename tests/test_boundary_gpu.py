@@ -129,6 +129,12 @@ def test_oneshot_zrt_render_rejects_bad_input():
     one, _ = native.render_oneshot(geo.scene, cam, 1, 4, device=99, devices=[0])
     ref, _ = native.render_oneshot(geo.scene, cam, 1, 4, device=0)
     assert np.array_equal(one, ref)
+    # num_devices 1 without a list keeps cfg.device (ABI-1 callers)
+    null1, _ = native.render_oneshot(geo.scene, cam, 1, 4, device=0, num_devices=1)
+    assert np.array_equal(null1, ref)
+    with pytest.raises(native.ZrtError) as e:
+        native.render_oneshot(geo.scene, cam, 1, 4, device=99, num_devices=1)
+    assert e.value.status == -2
 
 
 def _visible_gpus():

@@ -29,3 +29,7 @@ def test_brick_skip_matches_cell_walk(tmp_path, bm):
     import json
     res = json.loads(r.stdout)
     assert res["fails"] == 0 and res["walk_fails"] == 0 and res["walk_steps"] > 100000, res
+    # the packed-word checks ran on grids of this layout (for bm = 1
+    # the checker skips grids that do not pack brick-major, so zero counts
+    # would pass silently): brick skips, fast-forwards and their steps
+    assert res["layout_grids"] >= 10 and res["skipv"] > 1000 and res["ff"] > 1000 and res["ff_steps"] > 10000, res

@@ -129,6 +129,34 @@ def test_cfg2_whole_frame_vs_live_oracle(oracle_mod):
     _check_whole_frame("cfg2", rgb, lin, int(ctr[0]))
 
 
+def test_cfg1_whole_frame_vs_live_oracle(oracle_mod):
+    """cfg1 (BASELINE configs[0]: the sphere, 256^2, 1 spp):
+    the whole frame against a live oracle run (RGB8, linear radiance, the
+    traversal counters) and the committed whole-frame hashes, with the
+    default launch set and the counting build."""
+    d = scenes.CONFIGS["cfg1"]
+    soup = scenes.get_scene(d["scene"])
+    c = soup.camera(d["camera"])
+    cam = camera_for(soup, d["camera"], d["width"], d["height"])
+    rs = RenderScene(soup, device=0)
+    try:
+        img, res = rs.render(cam, num_samples=d["spp"], max_bounce=d["max_bounce"], linear=True)
+        cimg, cres = rs.render(cam, num_samples=d["spp"], max_bounce=d["max_bounce"], stats=True)
+    finally:
+        rs.close()
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, c.aspect, d["width"], d["height"])
+    rgb, lin, ctr = oracle_mod.OracleScene(soup).render(ocam, d["spp"], d["max_bounce"], oracle_mod.RNG_PATH, 0,
+                                                        _threads())
+    assert np.array_equal(img.reshape(-1, 3), rgb) and np.array_equal(cimg.reshape(-1, 3), rgb)
+    assert np.array_equal(_row_major(res["linear"], cam.w, cam.h).view(np.uint32), lin.view(np.uint32))
+    st = cres["stats"]
+    assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == tuple(int(x) for x in ctr[:4])
+    _check_whole_frame("cfg1", img.reshape(-1, 3), _row_major(res["linear"], cam.w, cam.h), res["stats"]["segments"])
+    g = GOLDEN["cfg1"]
+    assert (st["cells_visited"], st["triangle_tests"], st["hits"]) == \
+        (g["cells_visited"], g["triangle_tests"], g["hits"])
+
+
 def test_cfg4_on_a_repeated_device_group_whole_frame():
     """cfg4 (4K, 1024 spp: ~1 TB of path queues, many passes) split over a
     group that lists GPU 0 twice: the two contexts render side by side and
@@ -155,11 +183,14 @@ def test_cfg4_on_a_repeated_device_group_whole_frame():
 # never the result: each must reproduce the oracle's whole frame.  cfg3 runs
 # with the escape table by default and cfg5 without it (density), so between
 # them both park kernels and the plain primary are pinned at full size.
+# (round 6: mt_exact, the IEEE-division lane walk of the scenes with edges
+# of 2^62 or more; and cfg1, BASELINE configs[0], in every mode)
 MODES = {"escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
          "no_frustum": native.FLAG_NO_FRUSTUM, "one_set": native.FLAG_ONE_SET,
-         "lane_walk": native.FLAG_LANE_WALK}
-MODE_FRAMES = [(c, m) for c in ("cfg2", "cfg3") for m in MODES] + \
-    [("cfg5", "escape"), ("cfg5", "no_frustum"), ("cfg5", "lane_walk")]
+         "lane_walk": native.FLAG_LANE_WALK, "mt_exact": native.FLAG_MT_EXACT,
+         "frustum": native.FLAG_FRUSTUM}
+MODE_FRAMES = [(c, m) for c in ("cfg1", "cfg2", "cfg3") for m in MODES if not (c != "cfg1" and m == "frustum")] + \
+    [("cfg5", "escape"), ("cfg5", "no_frustum"), ("cfg5", "lane_walk"), ("cfg5", "mt_exact")]
 
 
 @pytest.fixture(scope="module")

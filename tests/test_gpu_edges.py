@@ -110,8 +110,10 @@ _ORACLE = {}
 # forced on / off (wf_park_kernel<true> / <false>) and the primary frustum
 # bounds forced on (small frames skip them by default): every one of them on
 # every degenerate grid (flat, 1x1x1, 3x5x2, coarse bricks, wide axes, sky)
+# ... and (round 6) the IEEE-division lane walk that scenes with edges of
+# 2^62 or more take (ZRT_FLAG_MT_EXACT forces it on any scene)
 MODES = {"default": 0, "escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
-         "frustum": native.FLAG_FRUSTUM}
+         "frustum": native.FLAG_FRUSTUM, "mt_exact": native.FLAG_MT_EXACT}
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -163,5 +165,56 @@ def test_growing_frames_counting_timed_counting(oracle_mod):
             for counting in (True, False, True):
                 img, _ = rs.render(cam, num_samples=spp, max_bounce=4, stats=counting)
                 assert np.array_equal(img.reshape(-1, 3), rgb), (w, h, spp, counting)
+    finally:
+        rs.close()
+
+
+def _far_vertex(scale):
+    """The sphere with one vertex moved to (scale, scale, scale): the
+    triangles around it get edge components near `scale` (Moller-Trumbore
+    dets up to ~scale^2, past the short reciprocal's 2^126 from 2^62 on)."""
+    s = scenes.get_scene("sphere")
+    pos = s.pos.astype(np.float32).copy()
+    pos[0, 0:3] = np.float32(scale)
+    return dataclasses.replace(s, name=f"far_vertex_{scale}", pos=pos)
+
+
+# (scale, needs the IEEE-division kernels)
+FAR = [(2.0 ** 40, False), (2.0 ** 62, True), (2.0 ** 64, True), (2.0 ** 100, True),
+       (float("inf"), True), (float("nan"), False)]
+
+
+@pytest.mark.parametrize("device_build", [False, True], ids=["host-build", "device-build"])
+@pytest.mark.parametrize("scale,exact", FAR, ids=[f"2^{int(np.log2(s))}" if np.isfinite(s) else str(s)
+                                                   for s, _ in FAR])
+def test_far_vertex_scene_renders_bitexact_vs_oracle(oracle_mod, scale, exact, device_build):
+    """the contexts no longer refuse scenes the reference
+    renders (linalg.zig:696-722 takes any f32).  A scene with an edge
+    component of 2^62 or more, or infinite, renders through the lane walk
+    with the IEEE division (the bounce launches are the wf_kernel class, no
+    park launch); image, linear radiance and counters equal the oracle's."""
+    soup = _far_vertex(scale)
+    w, h, spp, mb, res = 40, 32, 2, 4, (16, 16, 16)
+    cam = camera_for(soup, None, w, h)
+    c = soup.camera(None)
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
+    rgb, lin, ctr = oracle_mod.OracleScene(soup, res).render(ocam, spp, mb, oracle_mod.RNG_PATH, 0, 16)
+    pix = native.tile_pixels(cam.w, cam.h)
+    rs = RenderScene(soup, res, device_build=device_build)
+    try:
+        img, out = rs.render(cam, num_samples=spp, max_bounce=mb, stats=True, linear=True)
+        assert np.array_equal(img.reshape(-1, 3), rgb)
+        assert np.array_equal(out["linear"].view(np.uint32), lin[pix].view(np.uint32))
+        st = out["stats"]
+        assert (st["segments"], st["cells_visited"], st["triangle_tests"], st["hits"]) == \
+            tuple(int(x) for x in ctr[:4])
+        fast, fo = rs.render(cam, num_samples=spp, max_bounce=mb, linear=True)
+        kinds = rs.context.profile()["kernels"]
+        assert np.array_equal(fast.reshape(-1, 3), rgb)
+        assert np.array_equal(fo["linear"].view(np.uint32), lin[pix].view(np.uint32))
+        if exact:
+            assert "park" not in kinds and "bounce" in kinds, kinds
+        elif scale == 2.0 ** 40:
+            assert "park" in kinds, kinds
     finally:
         rs.close()

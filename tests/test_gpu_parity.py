@@ -38,7 +38,8 @@ def test_probe_triangle(oracle_mod, rng):
     c = (v[:, 0:3] + v[:, 3:6] + v[:, 6:9]) / 3
     d[: n // 2] = (c[: n // 2] - o[: n // 2])
     d = np.stack([_norm(x) for x in d])
-    # edge cases: axis-aligned, back face, det just below/above 1e-8, degenerate
+    # (the edge cases -- axis-aligned, back face, det at 1e-8, degenerate,
+    # edges beyond 2^62 -- are test_probe_triangle_edge_cases)
     inp = np.concatenate([v, o, d], 1).astype(np.float32)
     out = native.probe(native.PROBE_TRIANGLE, inp, n, (n, 4))
     flat = native.probe(native.PROBE_TRIANGLE_FLAT, inp, n, (n, 4))
@@ -73,6 +74,157 @@ def test_probe_triangle_culling_edges(oracle_mod):
         if h:
             assert np.array_equal(out[i, 1:], tuv)
     assert out[0, 0] == 1 and out[1, 0] == 0 and out[6, 0] == 0
+
+
+def _tri_edge_cases():
+    """(v0, v1, v2, orig, dir, in_domain) rows: in_domain = every edge
+    component below 2^62, where the park / packed kernels' short 1/det is
+    the division (zrt_math.h mt_inv_det)."""
+    f32 = np.float32
+    rows = []
+    unit = [0, 0, 0, 1, 0, 0, 0, 1, 0]
+    # axis-aligned rays along +-x, +-y, +-z at triangles facing each way
+    for ax in range(3):
+        b1, b2 = (ax + 1) % 3, (ax + 2) % 3
+        for sgn in (1.0, -1.0):
+            v0 = np.zeros(3); v1 = np.zeros(3); v2 = np.zeros(3)
+            v1[b1] = 1.0; v2[b2] = 1.0
+            if sgn < 0:
+                v1, v2 = v2, v1
+            o = np.full(3, 0.25); o[ax] = 2.0 * sgn
+            d = np.zeros(3); d[ax] = -sgn
+            rows.append((v0, v1, v2, o, d, True))
+            rows.append((v0, v1, v2, -o + 0.5, -d, True))           # from behind: back face
+    # det = e1 . (d x e2) = a * b exactly for e1 = (a,0,0), e2 = (0,b,0),
+    # d = (0,0,-1): just below, at and just above the 1e-8 culling threshold
+    th = f32(1e-8)
+    for det in (np.nextafter(th, f32(0)), th, np.nextafter(th, f32(1)), f32(2e-8), f32(0.0), f32(-1e-8)):
+        b = float(det)
+        rows.append(((0, 0, 0), (1, 0, 0), (0, b, 0), (0.25, b / 4, 1.0), (0, 0, -1), True))
+    # degenerate: zero area (one point), collinear, two equal vertices
+    rows.append(((0.2, 0.1, 0), (0.2, 0.1, 0), (0.2, 0.1, 0), (0.2, 0.1, 1), (0, 0, -1), True))
+    rows.append(((-0.5, 0, 0), (0, 0, 0), (0.5, 0, 0), (0, 0, 1), (0, 0, -1), True))
+    rows.append(((0.3, -0.4, 0), (0.3, -0.4, 0), (0.6, 0.2, 0), (0.4, -0.2, 1), (0, 0, -1), True))
+    # wide triangles: edges up to and beyond 2^62 (|det| up to 2^126 and past
+    # it, into the denormal reciprocals, and overflowing to inf)
+    for e in (40, 61, 62, 63, 64, 70, 100, 127):
+        s = float(2.0 ** e)
+        inside = e < 62
+        rows.append(((0, 0, 0), (s, 0, 0), (0, s, 0), (0.25, 0.25, 1), (0, 0, -1), inside))
+        rows.append(((-1, -1, 0), (s, 0, 0), (0, s, 0), (3.0, 5.0, 2.0), _norm([0.1, 0.2, -1]), inside))
+        rows.append(((-1, -1, -1), (s, s / 3, 0), (0, s, s / 5), (1.0, 2.0, 3.0), _norm([0.3, 0.2, -1]), inside))
+    for inf in (np.inf, -np.inf):
+        rows.append(((0, 0, 0), (inf, 0, 0), (0, 1, 0), (0.25, 0.25, 1), (0, 0, -1), False))
+        rows.append(((0, 0, 0), (1, 0, 0), (0, inf, 0), (0.25, 0.25, 1), (0, 0, -1), False))
+    rows.append(((0, 0, 0), (np.nan, 0, 0), (0, 1, 0), (0.25, 0.25, 1), (0, 0, -1), True))
+    return [(np.asarray(v0, f32), np.asarray(v1, f32), np.asarray(v2, f32), np.asarray(o, f32),
+             np.asarray(d, f32), dom) for v0, v1, v2, o, d, dom in rows]
+
+
+def _same_bits(a, b):
+    """Bit-equal f32 arrays, any NaN equal to any NaN (the sign and payload of
+    a NaN t / u / v never reach an image: `nearest > t and t > 0` rejects it,
+    stage3.zig:174-178)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    nan = np.isnan(a)
+    return np.array_equal(nan, np.isnan(b)) and np.array_equal(a[~nan].view(np.uint32), b[~nan].view(np.uint32))
+
+
+def test_probe_triangle_edge_cases(oracle_mod):
+    """Moller-Trumbore (linalg.zig:683-722) on the cases the reference's
+    culling and division meet: axis-aligned rays, back faces, det just
+    below / at / above 1e-8, zero and negative det, degenerate triangles and
+    wide ones (edges 2^40 .. 2^127, inf, NaN).  The IEEE-division test (the
+    kernels of the scenes with edges of 2^62 or more, ZRT_FLAG_MT_EXACT)
+    equals the oracle on every row; the short reciprocal (park and packed
+    kernels) and the branch-free form on every row inside its domain."""
+    rows = _tri_edge_cases()
+    inp = np.array([np.concatenate(r[:5]) for r in rows], np.float32)
+    n = len(rows)
+    exact = native.probe(native.PROBE_TRIANGLE_EXACT, inp, n, (n, 4))
+    short = native.probe(native.PROBE_TRIANGLE, inp, n, (n, 4))
+    flat = native.probe(native.PROBE_TRIANGLE_FLAT, inp, n, (n, 4))
+    hits = 0
+    for i, (v0, v1, v2, o, d, dom) in enumerate(rows):
+        h, tuv = oracle_mod.tri_intersect(v0, v1, v2, o, d)
+        hits += h
+        assert bool(exact[i, 0]) == h, (i, rows[i], exact[i])
+        if h:
+            assert _same_bits(exact[i, 1:], tuv), (i, exact[i], tuv)
+        if dom:
+            assert bool(short[i, 0]) == h, (i, rows[i], short[i])
+            assert flat[i, 0] == short[i, 0], i
+            if h:
+                assert _same_bits(short[i, 1:], tuv), (i, short[i], tuv)
+                assert _same_bits(flat[i, 1:], tuv), i
+    assert hits >= 12
+
+
+def _recip_inputs(rng, per_binade=2000):
+    """Seeded f32 dets: every binade 2^-95 .. 2^125 (per_binade mantissas,
+    both signs), the domain's edges and their neighbours, 1e-8 +- 1 ulp."""
+    f32 = np.float32
+    ex = np.repeat(np.arange(-95, 126), per_binade)
+    man = rng.integers(0, 1 << 23, ex.size)
+    bits = ((ex + 127).astype(np.uint32) << 23) | man.astype(np.uint32)
+    v = bits.view(f32)
+    edges = []
+    for x in (f32(2.0 ** -95), f32(2.0 ** 126), f32(1e-8), f32(2.0 ** -94), f32(2.0 ** 125)):
+        edges += [np.nextafter(x, f32(0)), x, np.nextafter(x, f32(np.inf))]
+    vals = np.concatenate([v, -v, np.array(edges, f32), -np.array(edges, f32)])
+    return vals
+
+
+def test_probe_recip_every_binade_vs_host_division(rng):
+    """The park / packed kernels' 1/det (v_rcp + six FMAs, zrt_math.h
+    mt_inv_det) against the host's IEEE f32 division, bit for bit, on 2,000
+    seeded mantissas of every binade of its domain 2^-95 < |det| < 2^126, both
+    signs, the domain's edges and neighbours and 1e-8 +- 1 ulp; the
+    IEEE-division kernels' form against the host on every class of float
+    (zero, denormals, the binades outside the domain, inf, NaN)."""
+    vals = _recip_inputs(rng)
+    n = vals.size
+    out = native.probe(native.PROBE_RECIP, vals, n, (n, 2))
+    with np.errstate(divide="ignore", over="ignore", under="ignore"):
+        host = (np.float32(1.0) / vals).astype(np.float32)
+    lo, hi = np.float32(2.0 ** -95), np.float32(2.0 ** 126)
+    dom = (np.abs(vals) > lo) & (np.abs(vals) < hi)
+    assert dom.sum() > 880_000
+    bad = np.flatnonzero(out[dom, 0].view(np.uint32) != host[dom].view(np.uint32))
+    assert bad.size == 0, (vals[dom][bad[:8]], out[dom, 0][bad[:8]], host[dom][bad[:8]])
+    # the IEEE form everywhere, incl. outside the domain and special values
+    extra = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1e-40, 2.0 ** -126, 2.0 ** 127,
+                      3.4e38, -3.4e38, 2.0 ** -96, 2.0 ** -100, 2.0 ** -127], np.float32)
+    allv = np.concatenate([vals, extra, (rng.integers(0, 1 << 32, 200_000, dtype=np.uint64)
+                                         .astype(np.uint32).view(np.float32))])
+    m = allv.size
+    out2 = native.probe(native.PROBE_RECIP, allv, m, (m, 2))
+    with np.errstate(all="ignore"):
+        host2 = (np.float32(1.0) / allv).astype(np.float32)
+    nan = np.isnan(host2)
+    assert np.array_equal(np.isnan(out2[:, 1]), nan)
+    assert np.array_equal(out2[~nan, 1].view(np.uint32), host2[~nan].view(np.uint32))
+
+
+def test_probe_recip_sweep_every_float_of_the_domain():
+    """Every f32 of 2^-95 < |det| < 2^126 (1.85 G values per sign), on the
+    device: the short reciprocal equals the device's IEEE division bit for
+    bit (which test_probe_recip_every_binade_vs_host_division pins to the
+    host's).  Outside the domain the two are reported, not required to agree."""
+    f32 = np.float32
+    b_lo = int(np.array(2.0 ** -95, f32).view(np.uint32)) + 1
+    b_hi = int(np.array(2.0 ** 126, f32).view(np.uint32))          # exclusive
+    ranges = []
+    for sign in (0, 1 << 31):
+        ranges.append((sign | b_lo, b_hi - b_lo))                   # the domain
+        ranges.append((sign, b_lo))                                 # 0 .. 2^-95 (denormals incl.)
+        ranges.append((sign | b_hi, 0x7F800000 - b_hi + 1))         # 2^126 .. inf
+    inp = np.array(ranges, np.uint32)
+    out = native.probe(native.PROBE_RECIP_SWEEP, inp, len(ranges), (len(ranges), 4), np.uint32)
+    for (start, cnt), (bad, first, _, _) in zip(ranges, out):
+        print(f"recip sweep [{start:#010x}, +{cnt}): {bad} mismatches, first {first:#010x}")
+    assert out[0, 0] == 0 and out[3, 0] == 0, out
+    assert out[0, 1] == 0xFFFFFFFF and out[3, 1] == 0xFFFFFFFF
 
 
 def _dda_probe(lo, hi, o, d, res):
@@ -337,17 +489,19 @@ def _look_camera(org, tgt, fov, w, h):
 
 
 @pytest.mark.parametrize("name", ["contest", "sponza", "cornell"])
-def test_frustum_bounds_random_cameras_identical(gpu_scenes, name):
+def test_frustum_bounds_random_cameras_identical(oracle_mod, gpu_scenes, name):
     """The primary launch's frustum bounds (escape.h frustum_bound: the
     fast-forward below lo, the stop past hi, the +inf blocks) against the
-    counting build, which walks every cell: random cameras inside and outside
-    the grid, wide and narrow, image sizes not multiples of the 8x8 block."""
+    oracle (it walks every cell, as the reference does) and
+    the counting build: random cameras inside and outside the grid, wide and
+    narrow, image sizes not multiples of the 8x8 block."""
     soup = scenes.get_scene(name)
     p = np.asarray(soup.pos, np.float64).reshape(-1, 3)
     lo, hi = p.min(0), p.max(0)
     ext = hi - lo
     rng = np.random.default_rng(7)
     rs = gpu_scenes(name)
+    osc = oracle_mod.OracleScene(soup)
     for k in range(6):
         inside = k % 2 == 0
         org = lo + ext * (rng.random(3) if inside else -1.0 + 3.0 * rng.random(3))
@@ -355,6 +509,14 @@ def test_frustum_bounds_random_cameras_identical(gpu_scenes, name):
         cam = _look_camera(org, tgt, rng.uniform(0.2, 1.6), 36 + 4 * k, 29 + 3 * k)
         ref, r0 = rs.render(cam, num_samples=3, max_bounce=2, stats=True, linear=True)
         img, r1 = rs.render(cam, num_samples=3, max_bounce=2, linear=True, flags=native.FLAG_FRUSTUM)
+        ocam = oracle_mod.camera_from_dict({"w": cam.w, "h": cam.h, "origin": list(cam.origin),
+                                            "llc": list(cam.lower_left_corner), "right": list(cam.right),
+                                            "up": list(cam.up)})
+        orgb, olin, octr = osc.render(ocam, 3, 2, oracle_mod.RNG_PATH, 0, 8)
+        pix = native.tile_pixels(cam.w, cam.h)
+        assert np.array_equal(img.reshape(-1, 3), orgb), (k, inside)
+        assert np.array_equal(r1["linear"].view(np.uint32), olin[pix].view(np.uint32)), k
+        assert r1["stats"]["segments"] == int(octr[0]), k
         assert np.array_equal(ref, img), (k, inside)
         assert np.array_equal(r0["linear"], r1["linear"]), k
         assert r0["stats"]["segments"] == r1["stats"]["segments"], k

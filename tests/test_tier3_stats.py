@@ -24,7 +24,9 @@ from zig_raytracing_contest_amd import RenderScene, camera_for, native, scenes
 
 K = 4
 SPP = 256
-CASES = [("cornell", None, 64, 64), ("contest", "Camera 1", 96, 54), ("sphere", None, 64, 64)]
+# (round 6: the Sponza-scale stand-in of cfg5 too)
+CASES = [("cornell", None, 64, 64), ("contest", "Camera 1", 96, 54), ("sphere", None, 64, 64),
+         ("sponza", None, 96, 54)]
 
 
 def _block_z(build, ref, h, w):

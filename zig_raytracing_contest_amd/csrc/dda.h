@@ -319,7 +319,9 @@ template <bool BM>
 ZHD uint32_t pk_add(uint32_t pc, uint32_t f, uint32_t d) {
     if (!BM) return pc + d;
     const uint32_t s = (uint32_t)((int32_t)d >> 31);
-#if defined(__HIP_DEVICE_COMPILE__) && ZRT_PK_BITOP3
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__) && ZRT_PK_BITOP3
+    // (v_bitop3 is a gfx950 instruction: an ARCH= build for another target
+    // takes the plain expression below)
     // g = (pc & f) | (~f & ~s) as ONE v_bitop3 (table index pc*4 + f*2 + s:
     // rows 0, 4, 6, 7 set); left to itself the compiler selects ~f by the
     // sign with a compare, a select and a v_not (6 VALU per step, not 4)

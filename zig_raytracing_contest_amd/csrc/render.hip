@@ -253,7 +253,7 @@ __device__ __forceinline__ bool first_active_lane() {
 // All triangles of one cell in reference order (stage3.zig:164-178), TB at
 // a time: the TB loads are issued before the first test so their latencies
 // overlap (one memory round trip per TB triangles instead of per triangle).
-template <int TB, bool STATS>
+template <int TB, bool STATS, bool MTX = false>
 __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint32_t e, v3 o, v3 d,
                                           float& nearest, float& hu, float& hv, uint32_t& hidx,
                                           uint32_t& n_tests, uint64_t* wstat) {
@@ -267,7 +267,7 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
             if (i + (uint32_t)k < e) {
                 if (STATS) ++n_tests;
                 float t, u, v;
-                if (tri_ray(A[k], B[k], Cc[k], o, d, &t, &u, &v)) {
+                if (tri_ray<MTX>(A[k], B[k], Cc[k], o, d, &t, &u, &v)) {
                     if (nearest > t && t > 0.0f) { nearest = t; hu = u; hv = v; hidx = i + k; }
                 }
             }
@@ -289,7 +289,7 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
 // TAU (packed walk): a frustum bound (escape.h frustum_bound lo) for this ray: the
 // crossings below it enter only empty cells; +inf: the ray meets no
 // occupied cell at all.
-template <bool STATS, int TB, bool PACKED = false, bool PK_BM = false>
+template <bool STATS, int TB, bool PACKED = false, bool PK_BM = false, bool MTX = false>
 __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t* occ, v3 o, v3 d,
                                            float& hu, float& hv, uint32_t& hidx, uint32_t& n_cells,
                                            uint32_t& n_tests, uint64_t* prof, uint32_t* wcnt = nullptr,
@@ -329,7 +329,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         for (;;) {
             if (occupied) {
                 const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
-                test_cell<TB, false>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+                test_cell<TB, false, MTX>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
                 lim = fminf(lim, nearest);                 // = min(nearest, far bound)
             }
             bool crossed, exited;
@@ -352,7 +352,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         if (occupied) {
             const uint2 cell = p.cells[s.lin];
             if (STATS) { prof[6] += 1; prof[7] += cell.y > cell.x ? 1 : 0; ncell = cell.y - cell.x; }
-            test_cell<TB, STATS>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8);
+            test_cell<TB, STATS, MTX>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof + 8);
         }
         if (STATS) {
             // wave-shared work of this trip: sum of the lanes' triangle counts
@@ -496,8 +496,10 @@ __global__ __launch_bounds__(kTraceBlock, 1) void trace_kernel(const TraceParams
             float hu = 0.0f, hv = 0.0f;
             uint32_t hidx = 0;
             const uint32_t c_before = n_cells, t_before = n_tests;
-            const float t = trace_ray<true, kTriBatch>(p, s_occ, o, d, hu, hv, hidx, n_cells, n_tests, prof,
-                                                       s_wcnt);
+            // (the plain IEEE division in Moller-Trumbore: the counting build is
+            // the timed kernels' checker and serves every scene, mt_inv_det)
+            const float t = trace_ray<true, kTriBatch, false, false, true>(p, s_occ, o, d, hu, hv, hidx, n_cells,
+                                                                           n_tests, prof, s_wcnt);
             if (slot == 0) { ++p_seg; p_cells += n_cells - c_before; p_tests += n_tests - t_before; }
             if (t == kInf) { L = env_color(d); break; }       // stage3.zig:195-197
             ++n_hits;
@@ -793,7 +795,9 @@ __device__ __forceinline__ void path_state(const WfParams& w, uint32_t i, uint32
 }
 
 // wf_kernel: one lane = one segment, walked and tested by the lane itself.
-template <int MINW, bool PRIMARY, bool PACKED, bool PK_BM = false>
+// MTX: Moller-Trumbore with the plain IEEE division (mt_inv_det), for the
+// scenes whose edges leave the short reciprocal's domain (zrt_context::mt_exact).
+template <int MINW, bool PRIMARY, bool PACKED, bool PK_BM = false, bool MTX = false>
 __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w) {
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
@@ -855,8 +859,8 @@ __global__ __launch_bounds__(kTraceBlock, MINW) void wf_kernel(const WfParams w)
             uint32_t hidx = 0;
             WF_STAMP(2);
             if (depth != 0)
-                t = trace_ray<false, kTriBatch, PACKED, PK_BM>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr, nullptr,
-                                                        tau, tfar);
+                t = trace_ray<false, kTriBatch, PACKED, PK_BM, MTX>(p, s_occ, o, d, hu, hv, hidx, dummy, dummy, nullptr,
+                                                                    nullptr, tau, tfar);
             WF_STAMP(0);
             uint32_t item, slot;
             Rng rng;
@@ -1225,7 +1229,15 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                                 ddav_from_t<PK_BM>(s0, gk, pk, s);
                                 if (ESC) {
                                     // (every DMA into this slot from the lane's last
-                                    // ray has landed: its kDone drained vmcnt above)
+                                    // ray has landed before this store: that ray's
+                                    // escape DMAs were issued before this refill's
+                                    // q_in loads, vector memory completes in order
+                                    // (vmcnt), and this store runs only after
+                                    // dda_init consumed o and d, i.e. after the
+                                    // compiler's wait for those loads.  With
+                                    // ZRT_PARK_LATE_DRAIN the kDone drain no longer
+                                    // sits between them; the parity suite renders
+                                    // every scene with the table forced on)
                                     const uint32_t bin = esc_dir_bin(d);
                                     eoff = (bin >> 5) * 4u;
                                     emask = w.esc && s0.neg < 8u ? 1u << (bin & 31u) : 0u;
@@ -1491,17 +1503,20 @@ __device__ __forceinline__ bool shade_continues(bool valid, float4 b, float4 h) 
 }
 // One entry (records loaded) shaded: an ending path writes its terminal
 // radiance; a continuing one is left in (o, d, item, depth, slot, rng, mask)
-// for the caller to store at its reserved position.
+// for the caller to store at its reserved position.  Returns shade_segment's
+// answer (false for an invalid entry), which must equal shade_continues':
+// the ZRT_SWEEP build counts disagreements (stats[60]) and fails the render
+// on any.
 struct ShadeOut {
     v3 o, d;
     uint32_t item, depth, slot, mask;
     Rng rng;
 };
-__device__ __forceinline__ void shade_entry_keep(const WfParams& w, const double* zx, const double* zf,
+__device__ __forceinline__ bool shade_entry_keep(const WfParams& w, const double* zx, const double* zf,
                                                  const DevMat* mats, bool valid, float4 a, float4 b, float4 c,
                                                  float4 h, const TriRec& tr, ShadeOut& so, uint32_t& n_seg,
                                                  unsigned long long* sp = nullptr) {
-    if (!valid) return;
+    if (!valid) return false;
     so.rng.s = ((uint64_t)__float_as_uint(c.y) << 32) | __float_as_uint(c.x);
     so.item = __float_as_uint(a.w);
     so.o = mk(a.x, a.y, a.z);
@@ -1511,9 +1526,10 @@ __device__ __forceinline__ void shade_entry_keep(const WfParams& w, const double
     so.mask = __float_as_uint(c.z);
     v3 L = mk(0, 0, 0);
     ++n_seg;
-    if (!shade_segment(w, zx, zf, mats, so.item, h.x, h.y, h.z, tr, so.o, so.d, so.depth, so.slot, so.rng, so.mask,
-                       L, sp))
-        w.term[so.item] = make_float4(L.x, L.y, L.z, __uint_as_float(so.mask));
+    const bool cont = shade_segment(w, zx, zf, mats, so.item, h.x, h.y, h.z, tr, so.o, so.d, so.depth, so.slot,
+                                    so.rng, so.mask, L, sp);
+    if (!cont) w.term[so.item] = make_float4(L.x, L.y, L.z, __uint_as_float(so.mask));
+    return cont;
 }
 
 // LMATS: the material descriptors (at most kLdsMats) copied to dynamic LDS
@@ -1597,8 +1613,14 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
 #pragma unroll
             for (int e = 0; e < kShadeEntries; ++e) {
                 ShadeOut so;
-                shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
-                                 tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so, n_seg, sp);
+                const bool cont = shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
+                                                   tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so,
+                                                   n_seg, sp);
+#ifdef ZRT_SWEEP
+                if (cont != pc[e]) atomicAdd(&p.stats[60], 1ull);
+#else
+                (void)cont;
+#endif
                 // (converged again: lane 0's reservation, long returned, reaches every lane)
                 const uint32_t base = __builtin_amdgcn_readfirstlane(ob) + region_base(w, grp) + before;
                 if (pc[e]) q_store(w, base + (uint32_t)__popcll(m[e] & below), so.o, so.d, so.item, so.depth, so.slot,
@@ -1764,6 +1786,11 @@ const WfFn kWfPrimaryBM = (WfFn)wf_kernel<kWfMinWaves0, true, true, true>;
 const WfFn kWfBounceBM = (WfFn)wf_kernel<kWfMinWaves, false, true, true>;
 const WfFn kWfPrimaryWide = (WfFn)wf_kernel<kWfMinWaves, true, false>;   // (6 waves: at 7 it spills)
 const WfFn kWfBounceWide = (WfFn)wf_kernel<kWfMinWaves, false, false>;
+// scenes with an edge component of 2^62 or more, or infinite
+// (zrt_context::mt_exact): the unpacked lane walk with the IEEE division in
+// Moller-Trumbore, for every launch
+const WfFn kWfPrimaryExact = (WfFn)wf_kernel<kWfMinWaves, true, false, false, true>;
+const WfFn kWfBounceExact = (WfFn)wf_kernel<kWfMinWaves, false, false, false, true>;
 
 // max_bounce picks the stack depth the counting kernel is compiled for.
 TraceFn count_fn(uint32_t max_bounce) {
@@ -1848,6 +1875,11 @@ struct zrt_context {
     double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
     bool occx_ok = false;
+    // an edge component of 2^62 or more, or infinite: every launch takes the
+    // lane walk with the IEEE division in Moller-Trumbore (kWf*Exact), since
+    // the park and packed kernels' short reciprocal holds for |det| < 2^126
+    // only (zrt_math.h mt_inv_det)
+    bool mt_exact = false;
     // grow-only work buffers
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;
     float4* d_out = nullptr; size_t out_cap = 0;     // counting build
@@ -1897,11 +1929,18 @@ static int validate_scene(const zrt_scene* s) {
     }
     for (uint32_t i = 0; i < s->num_triangles; ++i)
         if (s->triangles_material[i] >= s->num_materials) return ZRT_ERR_INVALID_ARG;
-    // edge components below 2^62 (the kernels' exact reciprocal of the
-    // Moller-Trumbore determinant holds below 2^126: zrt_math.h mt_inv_det)
-    for (uint64_t k = 0; k < 9ull * s->num_triangles; ++k)
-        if (k % 9 >= 3 && fabsf(s->triangles_pos[k]) >= 0x1p62f) return ZRT_ERR_UNSUPPORTED;
     return validate_materials(s);
+}
+
+// Whether a scene needs the IEEE-division kernels (zrt_context::mt_exact):
+// `n` floats of which those with k % stride in [first, stride) are checked
+// (baked refs: the e1, e2 components of v0 e1 e2; source triangles: every
+// vertex component, at 2^61, so that their differences stay below 2^62).
+// NaN components need nothing: both forms propagate them.
+static bool needs_mt_exact(const float* v, uint64_t n, uint32_t stride, uint32_t first, float lim) {
+    for (uint64_t k = 0; k < n; ++k)
+        if (k % stride >= first && fabsf(v[k]) >= lim) return true;
+    return false;
 }
 
 // Materials and texels only (textures inside the texel array).
@@ -1942,10 +1981,13 @@ extern "C" const char* zrt_timed_kernels(void) {
     // trace-only park kernel + the whole-wave shade kernel (or wf_kernel when
     // the scene's OccX does not fit the LDS)
     // (brick-major packed words, then field words: dda.h)
-    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb1EE,wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb0EE,"
+    // (the last bool of wf_kernel: MTX, the IEEE-division instantiations
+    // of the scenes with edges of 2^62 or more, not timed)
+    return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb1ELb0EE,wf_kernelILi" ZRT_STR(ZRT_WF_MINW0)
+           "ELb1ELb1ELb0ELb0EE,"
            "wf_park_kernelILb1ELb1E,wf_park_kernelILb0ELb1E,wf_park_kernelILb1ELb0E,wf_park_kernelILb0ELb0E,"
-           "wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(ZRT_WF_MINW) "ELb0ELb1ELb1EE,wf_kernelILi" ZRT_STR(
-               ZRT_WF_MINW) "ELb0ELb1ELb0EE";
+           "wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(ZRT_WF_MINW) "ELb0ELb1ELb1ELb0EE,wf_kernelILi" ZRT_STR(
+               ZRT_WF_MINW) "ELb0ELb1ELb0ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
 }
@@ -2163,6 +2205,7 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     c->ncells = s->num_cells;
     c->nrefs = s->num_triangles;
     c->nmat = s->num_materials;
+    c->mt_exact = needs_mt_exact(s->triangles_pos, 9ull * s->num_triangles, 9u, 3u, 0x1p62f);
     HIP_TRY(hipMalloc((void**)&c->d_cells, 8ull * c->ncells));
     HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
@@ -2575,11 +2618,10 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
     if (rc != ZRT_OK) return rc;
     for (uint32_t i = 0; i < num_triangles; ++i)
         if (material[i] >= num_materials) return ZRT_ERR_INVALID_ARG;
-    // vertex components below 2^61, so every edge component is below 2^62
-    // (validate_scene)
     if (num_triangles && !positions) return ZRT_ERR_INVALID_ARG;
-    for (uint64_t k = 0; k < 9ull * num_triangles; ++k)
-        if (fabsf(positions[k]) >= 0x1p61f) return ZRT_ERR_UNSUPPORTED;
+    // vertex components of 2^61 or more (or infinite) may give edge
+    // components of 2^62 or more: the IEEE-division kernels (mt_exact)
+    const bool mt_exact = needs_mt_exact(positions, 9ull * num_triangles, 1u, 0u, 0x1p61f);
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
     if (device < 0) {
@@ -2590,6 +2632,7 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
     zrt_context* c = new (std::nothrow) zrt_context();
     if (!c) return ZRT_ERR_OUT_OF_MEMORY;
     c->device = device;
+    c->mt_exact = mt_exact;
     rc = context_base(c);
     if (rc == ZRT_OK) {
         zrt::Grid grid;
@@ -2824,16 +2867,20 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     // spp, r02d).  ZRT_FLAG_LANE_WALK: wf_kernel for every launch (round 1's
     // path, and the fallback).
     // (the park walk packs a cell into one word: at most 1024 cells per axis)
+    // mtx: Moller-Trumbore with the IEEE division in every launch (scenes
+    // whose edges leave the short reciprocal's domain, or as the flag forces):
+    // the unpacked lane walk, kWf*Exact
+    const bool mtx = c->mt_exact || (cfg->flags & ZRT_FLAG_MT_EXACT);
     const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK) &&
-                           c->packed;
+                           c->packed && !mtx;
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
-    const bool packed = c->packed;
+    const bool packed = c->packed && !mtx;
     const bool pbm = packed && c->pk.bm;   // brick-major packed words (dda.h)
-    const WfFn f_first = packed ? (pbm ? kWfPrimaryBM : kWfPrimary) : kWfPrimaryWide;
+    const WfFn f_first = mtx ? kWfPrimaryExact : packed ? (pbm ? kWfPrimaryBM : kWfPrimary) : kWfPrimaryWide;
     // the escape table: where dense enough to pay (context_escape), or as
     // the flags force it (both kernels give the same image)
     // (built at the first frame of 2^23 samples or more, or the first the flag
@@ -2847,7 +2894,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                      (c->esc_on || (cfg->flags & ZRT_FLAG_ESCAPE));
     const WfFn f_next = park_next ? (pbm ? (esc ? (WfFn)wf_park_kernel<true, true> : (WfFn)wf_park_kernel<false, true>)
                                          : (esc ? (WfFn)wf_park_kernel<true, false> : (WfFn)wf_park_kernel<false, false>))
-                                  : (packed ? (pbm ? kWfBounceBM : kWfBounce) : kWfBounceWide);
+                                  : mtx ? kWfBounceExact : (packed ? (pbm ? kWfBounceBM : kWfBounce) : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
     const size_t lds_shade = c->nmat <= kLdsMats ? c->nmat * sizeof(DevMat) : 0;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
@@ -3137,6 +3184,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 "\"shared_rounds\": %llu}}\n",
                 hs[1], hs[4], hs[5], hs[2], hs[6], hs[7], hs[14], hs[15]);
 #ifdef ZRT_SWEEP
+    if (hs[60]) {       // the early append's reservation disagreed with shading (shade_entry_keep)
+        fprintf(stderr, "zrt: %llu shade continuations differ from their reservations\n", hs[60]);
+        return ZRT_ERR_HIP;
+    }
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_park_profile\": {\"cyc_shade_refill\": %llu, \"cyc_walk\": %llu, \"cyc_test\": %llu, "
                 "\"walk_iters\": %llu, \"walk_lanes\": %llu, \"test_rounds\": %llu, \"sub_rounds\": %llu, "
@@ -3231,10 +3282,10 @@ extern "C" int zrt_render(const zrt_scene* scene, const zrt_camera* cam, const z
         zrt_group_destroy(g);
         return rc;
     }
-    // a one-entry list names the device (it used to fall back to
-    // cfg->device silently)
-    if (cfg->num_devices == 1 && !cfg->devices) return ZRT_ERR_INVALID_ARG;
-    const int32_t dev = cfg->num_devices == 1 ? cfg->devices[0] : cfg->device;
+    // a one-entry list names the device; a null list keeps
+    // cfg->device, as ABI-1 callers that set num_devices = 1 for "one device"
+    // expect
+    const int32_t dev = cfg->num_devices == 1 && cfg->devices ? cfg->devices[0] : cfg->device;
     zrt_context* c = nullptr;
     int rc = zrt_context_create(scene, dev, &c);
     if (rc != ZRT_OK) return rc;
@@ -3264,6 +3315,15 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             const v3 v0 = ld3(a), v1 = ld3(a + 3), v2 = ld3(a + 6);
             float t = 0, u = 0, v = 0;
             const bool h = tri_ray(v0, sub(v1, v0), sub(v2, v0), ld3(a + 9), ld3(a + 12), &t, &u, &v);
+            o[0] = h ? 1.0f : 0.0f; o[1] = t; o[2] = u; o[3] = v;
+            break;
+        }
+        case ZRT_PROBE_TRIANGLE_EXACT: {  // the IEEE-division test of the mt_exact kernels
+            const float* a = (const float*)in + 15ull * i;
+            float* o = (float*)out + 4ull * i;
+            const v3 v0 = ld3(a), v1 = ld3(a + 3), v2 = ld3(a + 6);
+            float t = 0, u = 0, v = 0;
+            const bool h = tri_ray<true>(v0, sub(v1, v0), sub(v2, v0), ld3(a + 9), ld3(a + 12), &t, &u, &v);
             o[0] = h ? 1.0f : 0.0f; o[1] = t; o[2] = u; o[3] = v;
             break;
         }
@@ -3367,8 +3427,35 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             }
             break;
         }
+        case ZRT_PROBE_RECIP: {
+            const float x = ((const float*)in)[i];
+            float* o = (float*)out + 2ull * i;
+            o[0] = mt_inv_det<false>(x);
+            o[1] = mt_inv_det<true>(x);
+            break;
+        }
         default:
             break;
+    }
+}
+
+// ZRT_PROBE_RECIP_SWEEP: every float bit pattern of [lo, lo + count), the
+// short reciprocal against the IEEE division, bit for bit (NaN == NaN).
+__global__ __launch_bounds__(kBlock) void recip_sweep_kernel(uint32_t lo, uint32_t count, uint32_t* out) {
+    uint32_t bad = 0, first = 0xFFFFFFFFu;
+    for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < count; k += gridDim.x * kBlock) {
+        const float x = __uint_as_float(lo + k);
+        const float a = mt_inv_det<false>(x), b = mt_inv_det<true>(x);
+        const bool same = __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+        if (!same) { ++bad; first = min(first, lo + k); }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        bad += __shfl_xor(bad, o);
+        first = min(first, (uint32_t)__shfl_xor(first, o));
+    }
+    if ((threadIdx.x & 63u) == 0 && bad) {
+        atomicAdd(&out[0], bad);
+        atomicMin(&out[1], first);
     }
 }
 
@@ -3379,6 +3466,7 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
     size_t in_sz = 0, out_sz = 0, aux_sz = 0;
     switch (which) {
         case ZRT_PROBE_TRIANGLE:
+        case ZRT_PROBE_TRIANGLE_EXACT:
         case ZRT_PROBE_TRIANGLE_FLAT: in_sz = 60; out_sz = 16; break;
         case ZRT_PROBE_BBOX: in_sz = 48; out_sz = 8; break;
         case ZRT_PROBE_DDA: in_sz = 48; out_sz = 4 * (4 + 4 * 64); aux_sz = 12; break;
@@ -3386,6 +3474,8 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
         case ZRT_PROBE_RNG_F32:
         case ZRT_PROBE_RNG_NORM: in_sz = 12; out_sz = 64; break;
         case ZRT_PROBE_EXP_LOG: in_sz = 8; out_sz = 16; break;
+        case ZRT_PROBE_RECIP: in_sz = 4; out_sz = 8; break;
+        case ZRT_PROBE_RECIP_SWEEP: in_sz = 8; out_sz = 16; break;
         case ZRT_PROBE_TEXTURE: {
             in_sz = 8; out_sz = 12;
             if (!aux) return ZRT_ERR_INVALID_ARG;
@@ -3421,8 +3511,23 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
             HIP_TRY(hipMalloc(&d_aux, aux_sz));
             HIP_TRY(hipMemcpy(d_aux, aux, aux_sz, hipMemcpyHostToDevice));
         }
-        hipLaunchKernelGGL(probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d_in, d_out, n,
-                           d_aux, d_zig);
+        if (which == ZRT_PROBE_RECIP_SWEEP) {
+            const uint32_t* r = (const uint32_t*)in;
+            std::vector<uint32_t> init(4ull * n, 0u);
+            for (uint32_t k = 0; k < n; ++k) init[4ull * k + 1] = 0xFFFFFFFFu;
+            HIP_TRY(hipMemcpy(d_out, init.data(), out_sz * n, hipMemcpyHostToDevice));
+            for (uint32_t k = 0; k < n; ++k) {
+                if (r[2 * k + 1] == 0) continue;
+                if ((uint64_t)r[2 * k] + r[2 * k + 1] > 0x100000000ull) return ZRT_ERR_INVALID_ARG;
+                const uint32_t blocks = std::min<uint32_t>(8192u, (r[2 * k + 1] + kBlock - 1) / kBlock);
+                hipLaunchKernelGGL(recip_sweep_kernel, dim3(blocks), dim3(kBlock), 0, 0, r[2 * k], r[2 * k + 1],
+                                   (uint32_t*)d_out + 4ull * k);
+                HIP_TRY(hipGetLastError());
+            }
+        } else {
+            hipLaunchKernelGGL(probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d_in, d_out, n,
+                               d_aux, d_zig);
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipDeviceSynchronize());
         HIP_TRY(hipMemcpy(out, d_out, out_sz * n, hipMemcpyDeviceToHost));

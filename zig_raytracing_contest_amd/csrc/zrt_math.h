@@ -300,25 +300,32 @@ ZHD double rng_norm64(Rng& r, const double* zx, const double* zf) {
 // v_div_scale / v_div_fmas / v_div_fixup steps, which are identities for a
 // numerator of 1 and 2^-95 < |det| < 2^126 (no scaling, no special value):
 // 7 VALU instead of 11 (r05am).  A det below 1e-8 is rejected whatever this
-// returns, and |det| <= |e1| |e2| < 2^126 because the contexts take no
-// triangle with an edge component of 2^62 or more (validate_scene, NaN
-// aside, which both forms propagate).  A guard per wave instead split the
-// test loop and spilled.
+// returns, and |det| <= |e1| |e2| |d| < 2^126 for the kernels' unit
+// directions when every edge component is below 2^62 (NaN aside, which both
+// forms propagate).  Scenes with a larger or infinite edge component render
+// through the IEEE instantiation (IEEE = true: the plain division, every
+// operand) that the contexts select at creation (zrt_context::mt_exact):
+// a guard per wave instead split the test loop and spilled.  The device
+// probe ZRT_PROBE_RECIP_SWEEP checks the short form against the division
+// on every float of the domain (tests/test_gpu_parity.py).
+template <bool IEEE = false>
 ZHD float mt_inv_det(float det) {
 #if defined(__HIP_DEVICE_COMPILE__) && ZRT_MT_RCP
-    const float r = __builtin_amdgcn_rcpf(det);
-    const float f1 = __builtin_fmaf(__builtin_fmaf(-det, r, 1.0f), r, r);
-    const float f3 = __builtin_fmaf(__builtin_fmaf(-det, f1, 1.0f), f1, f1);
-    return __builtin_fmaf(__builtin_fmaf(-det, f3, 1.0f), f1, f3);
-#else
-    return 1.0f / det;
+    if (!IEEE) {
+        const float r = __builtin_amdgcn_rcpf(det);
+        const float f1 = __builtin_fmaf(__builtin_fmaf(-det, r, 1.0f), r, r);
+        const float f3 = __builtin_fmaf(__builtin_fmaf(-det, f1, 1.0f), f1, f1);
+        return __builtin_fmaf(__builtin_fmaf(-det, f3, 1.0f), f1, f3);
+    }
 #endif
+    return 1.0f / det;
 }
+template <bool IEEE = false>
 ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
     if (det < 0.00000001f) return false;
-    const float inv_det = mt_inv_det(det);
+    const float inv_det = mt_inv_det<IEEE>(det);
     const v3 tvec = sub(o, v0);
     const float u = dot(tvec, pvec) * inv_det;
     if (u < 0.0f || u > 1.0f) return false;
@@ -337,10 +344,11 @@ ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv
 // at the end, so for an accepted hit t, u and v are tri_ray's bit for bit, and
 // the hit/miss answer is tri_ray's for every input (a NaN passes a rejection
 // here exactly when tri_ray's `<` / `>` against it lets it continue).
+template <bool IEEE = false>
 ZHD bool tri_ray_flat(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
-    const float inv_det = mt_inv_det(det);
+    const float inv_det = mt_inv_det<IEEE>(det);
     const v3 tvec = sub(o, v0);
     const float u = dot(tvec, pvec) * inv_det;
     const v3 qvec = cross(tvec, e1);

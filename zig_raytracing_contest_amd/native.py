@@ -23,12 +23,14 @@ FLAG_COUNT_STATS, FLAG_LANE_WALK = 0x1, 0x2
 FLAG_ESCAPE, FLAG_NO_ESCAPE = 0x40, 0x80
 FLAG_FRUSTUM, FLAG_NO_FRUSTUM = 0x100, 0x200
 FLAG_ONE_SET, FLAG_KERNEL_TIMES = 0x10, 0x20
+FLAG_MT_EXACT = 0x400
 # zrt_kernel_profile classes (include/zrt.h)
 KERNEL_CLASSES = ("primary", "park", "shade", "bounce", "resolve", "count")
 
 PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
 PROBE_TRIANGLE_FLAT = 8
+PROBE_RECIP, PROBE_RECIP_SWEEP, PROBE_TRIANGLE_EXACT = 9, 10, 11
 DDA_PROBE_WIDTH = 4 + 4 * 64      # floats per ray: steps, first cell, 64 x (cell, t)
 
 
@@ -360,7 +362,7 @@ class Context:
 
 
 def render_oneshot(scene: Scene, cam: Camera, spp: int, max_bounce: int, seed: int = 0,
-                   device: int = -1, devices=None):
+                   device: int = -1, devices=None, num_devices=None):
     """zrt_render: the one-shot drop-in for Scene.render (stage3.zig:247) --
     upload, render the whole image, download, free.  `devices`: a list of
     HIP ordinals (repeats allowed) to split the image's tiles over
@@ -371,6 +373,8 @@ def render_oneshot(scene: Scene, cam: Camera, spp: int, max_bounce: int, seed: i
     if devices is not None:
         dl = (C.c_int32 * len(devices))(*devices)
         cfg.num_devices, cfg.devices = len(devices), dl
+    elif num_devices is not None:      # a count without a list (ABI-1 callers)
+        cfg.num_devices = num_devices
     img = np.zeros((cam.h, cam.w, 3), np.uint8)
     st = Stats()
     check(lib().zrt_render(C.byref(scene), C.byref(cam), C.byref(cfg), img.ctypes.data, C.byref(st)),
@@ -436,7 +440,8 @@ def timed_kernels():
 # bytes per item the probe reads / writes (render.hip zrt_probe)
 _PROBE_IO = {PROBE_TRIANGLE: (60, 16), PROBE_TRIANGLE_FLAT: (60, 16), PROBE_BBOX: (48, 8),
              PROBE_DDA: (48, 4 * DDA_PROBE_WIDTH), PROBE_TO_RGB: (12, 12), PROBE_RNG_F32: (12, 64),
-             PROBE_RNG_NORM: (12, 64), PROBE_EXP_LOG: (8, 16), PROBE_TEXTURE: (8, 12)}
+             PROBE_RNG_NORM: (12, 64), PROBE_EXP_LOG: (8, 16), PROBE_TEXTURE: (8, 12),
+             PROBE_RECIP: (4, 8), PROBE_RECIP_SWEEP: (8, 16), PROBE_TRIANGLE_EXACT: (60, 16)}
 
 
 def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=None, device=-1):
