@@ -179,21 +179,38 @@ def _far_vertex(scale):
     return dataclasses.replace(s, name=f"far_vertex_{scale}", pos=pos)
 
 
-# (scale, needs the IEEE-division kernels)
-FAR = [(2.0 ** 40, False), (2.0 ** 62, True), (2.0 ** 64, True), (2.0 ** 100, True),
-       (float("inf"), True), (float("nan"), False)]
+def _far_floor(scale):
+    """The sphere over a floor triangle with edges of 2 * scale, facing up
+    (y = -1.5): Moller-Trumbore's det for a ray down onto it is
+    4 scale^2 |d.y|, so from scale 2^62 on the bounce rays that hit it have
+    dets of 2^124 .. 2^128 and past (the short reciprocal's 2^126 limit, the
+    subnormal reciprocals, the overflow to inf)."""
+    s = scenes.get_scene("sphere")
+    S = np.float32(scale)
+    tri = np.array([[-S, -1.5, -S, 0, -1.5, S, S, -1.5, -S]], np.float32)
+    n = np.tile(np.array([0, 1, 0], np.float32), (1, 3))
+    return dataclasses.replace(s, name=f"far_floor_{scale}", pos=np.concatenate([s.pos, tri]),
+                               nrm=np.concatenate([s.nrm, n]), uv=np.concatenate([s.uv, np.zeros((1, 6), np.float32)]),
+                               mat=np.concatenate([s.mat, np.zeros(1, s.mat.dtype)]))
+
+
+# (scene, scale, needs the IEEE-division kernels)
+FAR = [("vertex", 2.0 ** 40, False), ("vertex", 2.0 ** 62, True), ("vertex", 2.0 ** 64, True),
+       ("vertex", 2.0 ** 100, True), ("vertex", float("inf"), True), ("vertex", float("nan"), False),
+       ("floor", 2.0 ** 40, False), ("floor", 2.0 ** 62, True), ("floor", 2.0 ** 63, True),
+       ("floor", 2.0 ** 64, True)]
 
 
 @pytest.mark.parametrize("device_build", [False, True], ids=["host-build", "device-build"])
-@pytest.mark.parametrize("scale,exact", FAR, ids=[f"2^{int(np.log2(s))}" if np.isfinite(s) else str(s)
-                                                   for s, _ in FAR])
-def test_far_vertex_scene_renders_bitexact_vs_oracle(oracle_mod, scale, exact, device_build):
+@pytest.mark.parametrize("kind,scale,exact", FAR, ids=[f"{k}-2^{int(np.log2(s))}" if np.isfinite(s) else f"{k}-{s}"
+                                                        for k, s, _ in FAR])
+def test_far_vertex_scene_renders_bitexact_vs_oracle(oracle_mod, kind, scale, exact, device_build):
     """the contexts no longer refuse scenes the reference
     renders (linalg.zig:696-722 takes any f32).  A scene with an edge
     component of 2^62 or more, or infinite, renders through the lane walk
     with the IEEE division (the bounce launches are the wf_kernel class, no
     park launch); image, linear radiance and counters equal the oracle's."""
-    soup = _far_vertex(scale)
+    soup = _far_vertex(scale) if kind == "vertex" else _far_floor(scale)
     w, h, spp, mb, res = 40, 32, 2, 4, (16, 16, 16)
     cam = camera_for(soup, None, w, h)
     c = soup.camera(None)
@@ -216,5 +233,7 @@ def test_far_vertex_scene_renders_bitexact_vs_oracle(oracle_mod, scale, exact, d
             assert "park" not in kinds and "bounce" in kinds, kinds
         elif scale == 2.0 ** 40:
             assert "park" in kinds, kinds
+        if kind == "floor":       # the floor is seen: hits beyond the sphere's
+            assert st["hits"] > 0
     finally:
         rs.close()

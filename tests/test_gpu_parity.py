@@ -113,6 +113,13 @@ def _tri_edge_cases():
         rows.append(((0, 0, 0), (s, 0, 0), (0, s, 0), (0.25, 0.25, 1), (0, 0, -1), inside))
         rows.append(((-1, -1, 0), (s, 0, 0), (0, s, 0), (3.0, 5.0, 2.0), _norm([0.1, 0.2, -1]), inside))
         rows.append(((-1, -1, -1), (s, s / 3, 0), (0, s, s / 5), (1.0, 2.0, 3.0), _norm([0.3, 0.2, -1]), inside))
+    # floor-like: e1 = (S, 0, 2S), e2 = (2S, 0, 0), rays down at d.y: det =
+    # 4 S^2 |d.y|, for S = 2^63 in [2^126, 2^128): subnormal reciprocals
+    for e in (62, 63):
+        S = float(2.0 ** e)
+        for dy in (-0.3, -0.6, -0.95):
+            d = _norm([0.1, dy, -0.2])
+            rows.append(((-S, 0, -S), (0, 0, S), (S, 0, -S), (0.5, 10.0, 0.25), d, e < 62))
     for inf in (np.inf, -np.inf):
         rows.append(((0, 0, 0), (inf, 0, 0), (0, 1, 0), (0.25, 0.25, 1), (0, 0, -1), False))
         rows.append(((0, 0, 0), (1, 0, 0), (0, inf, 0), (0.25, 0.25, 1), (0, 0, -1), False))
@@ -144,13 +151,15 @@ def test_probe_triangle_edge_cases(oracle_mod):
     exact = native.probe(native.PROBE_TRIANGLE_EXACT, inp, n, (n, 4))
     short = native.probe(native.PROBE_TRIANGLE, inp, n, (n, 4))
     flat = native.probe(native.PROBE_TRIANGLE_FLAT, inp, n, (n, 4))
-    hits = 0
+    hits = outside_differs = 0
     for i, (v0, v1, v2, o, d, dom) in enumerate(rows):
         h, tuv = oracle_mod.tri_intersect(v0, v1, v2, o, d)
         hits += h
         assert bool(exact[i, 0]) == h, (i, rows[i], exact[i])
         if h:
             assert _same_bits(exact[i, 1:], tuv), (i, exact[i], tuv)
+        if not dom and not (bool(short[i, 0]) == h and (not h or _same_bits(short[i, 1:], tuv))):
+            outside_differs += 1
         if dom:
             assert bool(short[i, 0]) == h, (i, rows[i], short[i])
             assert flat[i, 0] == short[i, 0], i
@@ -158,6 +167,10 @@ def test_probe_triangle_edge_cases(oracle_mod):
                 assert _same_bits(short[i, 1:], tuv), (i, short[i], tuv)
                 assert _same_bits(flat[i, 1:], tuv), i
     assert hits >= 12
+    # outside its domain the short reciprocal does give other answers (the
+    # subnormal 1/det of the 2^63 floor rows): the IEEE kernels are needed
+    print(f"rows outside the domain where the short form differs: {outside_differs}")
+    assert outside_differs >= 1
 
 
 def _recip_inputs(rng, per_binade=2000):
