@@ -22,9 +22,10 @@ LIB       := $(PKG)/libzrt.so
 CLI       := $(PKG)/bin/zrt
 
 PROBE     := tools/bin/dpp_probe
+INITPROBE := tools/bin/hip_init_probe
 SWEEP_LIB := tools/bin/sweep/libzrt.so
 
-all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) $(PROBE) $(SWEEP_LIB) oracle
+all: $(LIB) $(if $(wildcard $(SRC)/cli.cpp),$(CLI)) $(PROBE) $(INITPROBE) $(SWEEP_LIB) oracle
 
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) $(wildcard $(SRC)/*.h)
 	@mkdir -p $(OBJ)
@@ -47,6 +48,11 @@ $(CLI): $(SRC)/cli.cpp $(LIB) include/zrt.h
 $(PROBE): tools/dpp_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
+
+# HIP start-up split (tools/startup_probe.py)
+$(INITPROBE): tools/hip_init_probe.cpp
+	@mkdir -p tools/bin
+	$(HIPCC) -O2 -o $@ $< -ldl
 
 # Tuning build: the park-kernel schedule read from ZRT_PARK_T / ZRT_PARK_R,
 # ZRT_SETS, and the s_memtime round profiles (ZRT_PARK_PROFILE); used through

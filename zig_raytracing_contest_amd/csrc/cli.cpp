@@ -129,7 +129,16 @@ int main(int argc, char** argv) {
     // first GPU use
     int warm_dev = 0;
     if (const char* e = getenv("ZRT_DEVICES")) warm_dev = atoi(e);
-    std::thread hip_warm([warm_dev] { (void)zrt_device_warmup(warm_dev); });
+    // ZRT_TIMING=1: the start-up split on stderr ("timing:" lines, not the
+    // reference's phase lines): when the warm-up thread ran, how long the
+    // first GPU use waited for it, the group creation and the grid info
+    const bool timing = getenv("ZRT_TIMING") != nullptr;
+    uint64_t warm_begin_ns = 0, warm_end_ns = 0;
+    std::thread hip_warm([warm_dev, t_start, &warm_begin_ns, &warm_end_ns] {
+        warm_begin_ns = since(t_start);
+        (void)zrt_device_warmup(warm_dev);
+        warm_end_ns = since(t_start);
+    });
     struct Join {
         std::thread& t;
         ~Join() { if (t.joinable()) t.join(); }
@@ -230,14 +239,24 @@ int main(int argc, char** argv) {
         const int mode = db ? atoi(db) : 2;
         uint32_t empty = 0, mn = 0xFFFFFFFFu, mx = 0, ncells = 0, nrefs = 0;
         if (mode == 2) {
+            const uint64_t join0 = since(t_start);
             if (hip_warm.joinable()) hip_warm.join();
+            const uint64_t join1 = since(t_start);
             rc = zrt_group_create_built(pos, nrm, uv, mat, ntri, cfg.res, scene.num_materials, scene.materials,
                                         scene.texels, scene.num_texel_floats, devices.data(), ndev, &group);
             if (rc != ZRT_OK) return fail("Geometry.build", rc);
+            const uint64_t built = since(t_start);
             zrt_context* c0 = nullptr;
             uint32_t gi[4];
             if ((rc = zrt_group_context(group, 0, &c0)) != ZRT_OK || (rc = zrt_context_grid_info(c0, nullptr, gi)) != ZRT_OK)
                 return fail("Geometry.build", rc);
+            if (timing)
+                fprintf(stderr, "timing: warm-up thread %s .. %s (%s), joined at %s after waiting %s, "
+                        "group_create_built %s, grid info %s\n",
+                        fmt_duration(warm_begin_ns).c_str(), fmt_duration(warm_end_ns).c_str(),
+                        fmt_duration(warm_end_ns - warm_begin_ns).c_str(), fmt_duration(join1).c_str(),
+                        fmt_duration(join1 - join0).c_str(), fmt_duration(built - join1).c_str(),
+                        fmt_duration(since(t_start) - built).c_str());
             ncells = cfg.res[0] * cfg.res[1] * cfg.res[2];
             nrefs = gi[0]; empty = gi[1]; mn = gi[2]; mx = gi[3];
         } else {

@@ -60,7 +60,7 @@ struct DevGuard {
 struct zrt_group {
     std::vector<int> devices;
     std::vector<zrt_context*> ctx;
-    hipStream_t stream = nullptr;              // on devices[0]: the gather
+    hipStream_t stream = nullptr;              // on devices[0]: the gather (the first context's, not owned)
     uint8_t* d_gather = nullptr; size_t gather_cap = 0;   // every device's packed tiles, device order
     uint8_t* d_img = nullptr; size_t img_cap = 0;
     uint32_t* d_pix = nullptr; size_t pix_cap = 0;        // their pixel indices, same order
@@ -114,8 +114,9 @@ int group_create(const int32_t* devices, uint32_t n, zrt_group** out, Make make)
                 (void)hipGetLastError();   // clear an "already enabled" status
             }
         }
-        if (rc == ZRT_OK && hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess)
-            rc = ZRT_ERR_HIP;
+        // the gather runs on the first context's stream (on devices[0]; idle
+        // once its render has returned): no stream of the group's own
+        if (rc == ZRT_OK) g->stream = (hipStream_t)zrt::context_stream(g->ctx[0]);
     }
     if (rc != ZRT_OK) {
         zrt_group_destroy(g);
@@ -171,7 +172,6 @@ extern "C" void zrt_group_destroy(zrt_group* g) {
         if (g->d_gather) (void)hipFree(g->d_gather);
         if (g->d_img) (void)hipFree(g->d_img);
         if (g->d_pix) (void)hipFree(g->d_pix);
-        if (g->stream) (void)hipStreamDestroy(g->stream);
     }
     delete g;
 }
@@ -225,7 +225,8 @@ extern "C" int zrt_group_render(zrt_group* g, const zrt_camera* cam, const zrt_r
             }
             if (off != npx) return ZRT_ERR_INVALID_ARG;
             if ((rc = grow_on(&g->d_pix, &g->pix_cap, npx)) != ZRT_OK) return rc;
-            GROUP_TRY(hipMemcpy(g->d_pix, all.data(), npx * 4, hipMemcpyHostToDevice));
+            GROUP_TRY(hipMemcpyAsync(g->d_pix, all.data(), npx * 4, hipMemcpyHostToDevice, g->stream));
+            GROUP_TRY(hipStreamSynchronize(g->stream));
             memcpy(g->pix_key, key, sizeof key);
             g->pix_valid = true;
         }

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <new>
 #include <vector>
 
@@ -654,6 +655,14 @@ __device__ __forceinline__ TriRec tri_rec(const TraceParams& p, float t, uint32_
     r.d0 = tdp[0]; r.d1 = tdp[1]; r.d2 = tdp[2]; r.d3 = tdp[3];
     return r;
 }
+// LAST: the segment is the path's last (depth 1, the last bounce launch):
+// traceRayRecursive at depth 1 returns e + a * (the depth-0 call's 0) on a
+// scatter and 0 on a pass-through (stage3.zig:188-219), so the terminal
+// radiance is e + a * 0 itself -- the resolve's fold step add(e, mul(a, L))
+// at L = 0, the same f32 operations, with e = +0 exactly when the material
+// emits nothing -- and no bounce plane, scatter bit, normal draws (the
+// ziggurat) or queue append is needed.
+template <bool LAST = false>
 __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* zx, const double* zf,
                                               const DevMat* mats, uint32_t item, float t, float hu, float hv,
                                               const TriRec& tr, v3& o, v3& d, uint32_t& depth, uint32_t& slot,
@@ -677,6 +686,13 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
     const v3 no = add(o, scale(d, t + kFltEps));
     const float u_tr = rng_float(rng);
     SHADE_STAMP(4, u_tr);                                   // transparency draw
+    if (LAST) {
+        // the fold's last step at L = 0 (ZRT_PLANES16: e = +0 exactly when no
+        // e was stored, i.e. when every bit of the sampled e is zero: then
+        // the sample is that +0)
+        L = !(u_tr > transparency) ? add(emissive, mul(albedo, mk(0.0f, 0.0f, 0.0f))) : mk(0, 0, 0);
+        return false;
+    }
     if (!(u_tr > transparency)) {                           // stage3.zig:207, :214-219
         // the (e, a) pair goes out before the normal draws, so the ziggurat
         // (f64, 64-bit RNG) runs without the six colour registers live; 24 B
@@ -1498,6 +1514,21 @@ __device__ __forceinline__ void shade_entry(const WfParams& w, const double* zx,
 #ifndef ZRT_SHADE_EARLY_APPEND
 #define ZRT_SHADE_EARLY_APPEND 1
 #endif
+#ifndef ZRT_SHADE_LAST
+#define ZRT_SHADE_LAST 1
+#endif
+// its entries per lane per fetch and launch bound: r06f, 3 rounds of
+// alternating processes at full spp, images identical, against no LAST
+// kernel (6518 / 3851 / 4165 Mrays/s cfg3 / cfg5 / cfg2): 4 entries (78
+// VGPRs) 6586 / 3859 / 4193 (+1.0 / +0.2 / +0.7%); 3 entries (65) 6580 /
+// 3845 / 4170; 2 entries at 8 waves per SIMD (52 VGPRs: two waves fit beside
+// four park waves) 6564 / 3832 / 4123 (profiles/r06/r06f_ab_shade_last.log)
+#ifndef ZRT_SHADE_LAST_MINW
+#define ZRT_SHADE_LAST_MINW 1
+#endif
+#ifndef ZRT_SHADE_LAST_N
+#define ZRT_SHADE_LAST_N 4
+#endif
 __device__ __forceinline__ bool shade_continues(bool valid, float4 b, float4 h) {
     return valid && h.x != kInf && (__float_as_uint(b.w) & 0xFFFFu) >= 2u;
 }
@@ -1512,6 +1543,7 @@ struct ShadeOut {
     uint32_t item, depth, slot, mask;
     Rng rng;
 };
+template <bool LAST = false>
 __device__ __forceinline__ bool shade_entry_keep(const WfParams& w, const double* zx, const double* zf,
                                                  const DevMat* mats, bool valid, float4 a, float4 b, float4 c,
                                                  float4 h, const TriRec& tr, ShadeOut& so, uint32_t& n_seg,
@@ -1526,8 +1558,8 @@ __device__ __forceinline__ bool shade_entry_keep(const WfParams& w, const double
     so.mask = __float_as_uint(c.z);
     v3 L = mk(0, 0, 0);
     ++n_seg;
-    const bool cont = shade_segment(w, zx, zf, mats, so.item, h.x, h.y, h.z, tr, so.o, so.d, so.depth, so.slot,
-                                    so.rng, so.mask, L, sp);
+    const bool cont = shade_segment<LAST>(w, zx, zf, mats, so.item, h.x, h.y, h.z, tr, so.o, so.d, so.depth,
+                                          so.slot, so.rng, so.mask, L, sp);
     if (!cont) w.term[so.item] = make_float4(L.x, L.y, L.z, __uint_as_float(so.mask));
     return cont;
 }
@@ -1538,11 +1570,14 @@ __device__ __forceinline__ bool shade_entry_keep(const WfParams& w, const double
 // hit -> triangle data -> material -> texels takes its material hop from LDS
 // instead of L2.
 constexpr uint32_t kLdsMats = 64;
-template <bool LMATS>
+// LAST: the launch of a pass's last bounce (every entry has depth 1): the
+// terminal radiance only (shade_segment<true>), no append (ZRT_SHADE_LAST)
+template <bool LMATS, bool LAST = false>
 #ifndef ZRT_SHADE_MINW
 #define ZRT_SHADE_MINW 1
 #endif
-__global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(const WfParams w) {
+__global__ __launch_bounds__(kTraceBlock, LAST ? ZRT_SHADE_LAST_MINW : ZRT_SHADE_MINW) void wf_shade_kernel(const WfParams w) {
+    constexpr int NE = LAST ? ZRT_SHADE_LAST_N : kShadeEntries;   // entries per lane per fetch
     const TraceParams& p = w.t;
     __shared__ double s_zig[514];
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dynm[];    // LMATS: p.nmat DevMat
@@ -1573,19 +1608,19 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
 #else
     unsigned long long* const sp = nullptr;
 #endif
-    // kShadeEntries entries per lane per fetch: every entry's records are
+    // NE entries per lane per fetch: every entry's records are
     // loaded before the first is shaded, so their latency overlaps the
     // earlier entries' dependent chains (2: cfg3 +1.2%, cfg2 / cfg5 within
     // noise, 112 VGPRs, r02c6)
     for (;;) {
         uint32_t base = 0, lim = 0;
-        if (!wf_fetch<false>(ws, 64u * kShadeEntries, grp, tried, base, lim)) break;
+        if (!wf_fetch<false>(ws, 64u * NE, grp, tried, base, lim)) break;
         SHADE_STAMP(0, base);                  // work atomic
-        float4 a[kShadeEntries], b[kShadeEntries], c[kShadeEntries], h[kShadeEntries];
-        bool hit[kShadeEntries];
+        float4 a[NE], b[NE], c[NE], h[NE];
+        bool hit[NE];
         {
 #pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) {
+            for (int e = 0; e < NE; ++e) {
                 const uint32_t j = base + 64u * e + lane;
                 a[e] = b[e] = c[e] = h[e] = z4;
                 hit[e] = j < lim;
@@ -1595,12 +1630,20 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
                 }
             }
         }
-        if (ZRT_SHADE_EARLY_APPEND) {
-            bool pc[kShadeEntries];
-            uint64_t m[kShadeEntries];
+        if (LAST) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                ShadeOut so;
+                (void)shade_entry_keep<true>(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
+                                             tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so, n_seg,
+                                             sp);
+            }
+        } else if (ZRT_SHADE_EARLY_APPEND) {
+            bool pc[NE];
+            uint64_t m[NE];
             uint32_t tot = 0;
 #pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) {
+            for (int e = 0; e < NE; ++e) {
                 pc[e] = shade_continues(hit[e], b[e], h[e]);
                 m[e] = __ballot(pc[e]);
                 tot += (uint32_t)__popcll(m[e]);
@@ -1611,7 +1654,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
             // (each entry's triangle record loaded as its shading starts: all
             // of them up front took 100 VGPRs and lost co-residency, r05c)
 #pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e) {
+            for (int e = 0; e < NE; ++e) {
                 ShadeOut so;
                 const bool cont = shade_entry_keep(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
                                                    tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), so,
@@ -1629,7 +1672,7 @@ __global__ __launch_bounds__(kTraceBlock, ZRT_SHADE_MINW) void wf_shade_kernel(c
             }
         } else {
 #pragma unroll
-            for (int e = 0; e < kShadeEntries; ++e)
+            for (int e = 0; e < NE; ++e)
                 shade_entry(w, zx, zf, mats, hit[e], a[e], b[e], c[e], h[e],
                             tri_rec(p, hit[e] ? h[e].x : kInf, __float_as_uint(h[e].w)), below, grp, n_seg, sp);
         }
@@ -1917,6 +1960,36 @@ struct zrt_context {
 
 static int validate_materials(const zrt_scene* s);
 
+// A copy on the context's stream, waited for: the product path never uses
+// HIP's null stream, whose first use in a process creates its hardware
+// queue (~10 ms of the CLI's start-up, r06d)
+static hipError_t copy_sync(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st) {
+    const hipError_t e = hipMemcpyAsync(dst, src, n, kind, st);
+    return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+
+// ZRT_TIMING=1: context creation's stages on stderr ("timing:" lines), each
+// closed by a stream sync (the start-up split of VERDICT r5 #6)
+struct StageClock {
+    bool on = getenv("ZRT_TIMING") != nullptr;
+    double t = 0.0;
+    static double now_ms() {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+    }
+    StageClock() { t = now_ms(); }
+    void mark(const zrt_context* c, const char* what);
+};
+
+void StageClock::mark(const zrt_context* c, const char* what) {
+    if (!on) return;
+    (void)hipStreamSynchronize(c->stream);
+    const double n = now_ms();
+    fprintf(stderr, "timing: context %s %.3f ms\n", what, n - t);
+    t = n;
+}
+
 static int validate_scene(const zrt_scene* s) {
     if (!s) return ZRT_ERR_INVALID_ARG;
     const uint64_t nc = (uint64_t)s->grid.resolution[0] * s->grid.resolution[1] * s->grid.resolution[2];
@@ -1986,7 +2059,7 @@ extern "C" const char* zrt_timed_kernels(void) {
     return "wf_kernelILi" ZRT_STR(ZRT_WF_MINW0) "ELb1ELb1ELb1ELb0EE,wf_kernelILi" ZRT_STR(ZRT_WF_MINW0)
            "ELb1ELb1ELb0ELb0EE,"
            "wf_park_kernelILb1ELb1E,wf_park_kernelILb0ELb1E,wf_park_kernelILb1ELb0E,wf_park_kernelILb0ELb0E,"
-           "wf_shade_kernelILb1E,wf_kernelILi" ZRT_STR(ZRT_WF_MINW) "ELb0ELb1ELb1ELb0EE,wf_kernelILi" ZRT_STR(
+           "wf_shade_kernelILb1ELb0EE,wf_shade_kernelILb1ELb1EE,wf_kernelILi" ZRT_STR(ZRT_WF_MINW) "ELb0ELb1ELb1ELb0EE,wf_kernelILi" ZRT_STR(
                ZRT_WF_MINW) "ELb0ELb1ELb0ELb0EE";
 #undef ZRT_STR
 #undef ZRT_STR2
@@ -1996,15 +2069,27 @@ extern "C" const char* zrt_timed_kernels(void) {
 // the library's code objects (one fat binary, loaded on first use: ~0.1-0.2 s
 // on MI355X).  Lets a host overlap it with file loading.
 extern "C" int zrt_device_warmup(int device) {
+    // ZRT_TIMING: the split of the HIP start-up (runtime initialisation,
+    // device context, the two code objects) on stderr
+    const bool timing = getenv("ZRT_TIMING") != nullptr;
+    const double t0 = StageClock::now_ms();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ZRT_ERR_NO_DEVICE;
+    const double t1 = StageClock::now_ms();
     if (device < 0) device = 0;
     if (device >= n) return ZRT_ERR_NO_DEVICE;
     DeviceGuard g(device);
     HIP_TRY(hipFree(nullptr));
+    const double t2 = StageClock::now_ms();
     hipFuncAttributes fa;
     HIP_TRY(hipFuncGetAttributes(&fa, (const void*)resolve_kernel));
-    return grid_build_warmup();
+    const double t3 = StageClock::now_ms();
+    const int rc = grid_build_warmup();
+    if (timing)
+        fprintf(stderr, "timing: warm-up: runtime init (hipGetDeviceCount) %.3f ms, device context %.3f ms, "
+                "render.hip code object %.3f ms, grid_build.hip code object %.3f ms\n",
+                t1 - t0, t2 - t1, t3 - t2, StageClock::now_ms() - t3);
+    return rc;
 }
 
 extern "C" void zrt_context_destroy(zrt_context* c) {
@@ -2093,12 +2178,16 @@ __global__ __launch_bounds__(1024) void occx_pack_kernel(const uint32_t* __restr
 }  // namespace
 
 static int context_base(zrt_context* c) {
+    StageClock sc;
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    sc.mark(c, "stream");
     HIP_TRY(hipEventCreate(&c->ev_begin));
     HIP_TRY(hipEventCreate(&c->ev_end));
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, c->device));
-    c->num_cus = prop.multiProcessorCount;
+    sc.mark(c, "events");
+    // one attribute, not hipGetDeviceProperties (which fills ~100 fields and
+    // took ~10 ms of the CLI's start-up, r06c)
+    HIP_TRY(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    sc.mark(c, "CU count");
     return ZRT_OK;
 }
 
@@ -2191,8 +2280,10 @@ static int context_packed(zrt_context* c) {
 }
 
 static int context_counters(zrt_context* c) {
+    StageClock sc;
     int rc = context_packed(c);
     if (rc != ZRT_OK) return rc;
+    sc.mark(c, "cell records (cell32_kernel)");
     HIP_TRY(hipMalloc((void**)&c->d_counter, 64));
     HIP_TRY(hipMalloc((void**)&c->d_stats, 512));
     return ZRT_OK;
@@ -2207,7 +2298,7 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
     c->nmat = s->num_materials;
     c->mt_exact = needs_mt_exact(s->triangles_pos, 9ull * s->num_triangles, 9u, 3u, 0x1p62f);
     HIP_TRY(hipMalloc((void**)&c->d_cells, 8ull * c->ncells));
-    HIP_TRY(hipMemcpy(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_cells, s->cells, 8ull * c->ncells, hipMemcpyHostToDevice, c->stream));
     const size_t nr = std::max<size_t>(c->nrefs, 1);
     std::vector<float> pos(kTriFloats * nr, 0.0f);
     std::vector<float4> dat(4 * nr);
@@ -2221,9 +2312,9 @@ static int context_init(zrt_context* c, const zrt_scene* s) {
         memcpy(&dat[4 * i], tmp, 64);
     }
     HIP_TRY(hipMalloc((void**)&c->d_pos, pos.size() * sizeof(float)));
-    HIP_TRY(hipMemcpy(c->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_pos, pos.data(), pos.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMalloc((void**)&c->d_data, dat.size() * sizeof(float4)));
-    HIP_TRY(hipMemcpy(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_data, dat.data(), dat.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     if ((rc = context_materials(c, s)) != ZRT_OK) return rc;
     return context_occupancy(c, s->cells);
 }
@@ -2245,14 +2336,19 @@ static int context_materials(zrt_context* c, const zrt_scene* s) {
             dev_tex_inline(d, s->texels, k < 2 ? 3 : 1);
         }
     }
+    StageClock sc;
     HIP_TRY(hipMalloc((void**)&c->d_mats, mats.size() * sizeof(DevMat)));
-    HIP_TRY(hipMemcpy(c->d_mats, mats.data(), mats.size() * sizeof(DevMat), hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_mats, mats.data(), mats.size() * sizeof(DevMat), hipMemcpyHostToDevice, c->stream));
+    sc.mark(c, "materials");
     HIP_TRY(hipMalloc((void**)&c->d_texels, s->num_texel_floats * sizeof(float)));
-    HIP_TRY(hipMemcpy(c->d_texels, s->texels, s->num_texel_floats * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_texels, s->texels, s->num_texel_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    sc.mark(c, "texels");
     double zig[514];
     zig_tables(zig, zig + 257);
+    sc.mark(c, "ziggurat tables (host)");
     HIP_TRY(hipMalloc((void**)&c->d_zig, sizeof zig));
-    HIP_TRY(hipMemcpy(c->d_zig, zig, sizeof zig, hipMemcpyHostToDevice));
+    HIP_TRY(copy_sync(c->d_zig, zig, sizeof zig, hipMemcpyHostToDevice, c->stream));
+    sc.mark(c, "ziggurat upload");
     return ZRT_OK;
 }
 
@@ -2447,6 +2543,7 @@ static int context_escape(zrt_context* c) {
 }
 
 static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
+    StageClock sc_occ;
     const uint32_t* r = c->grid.resolution;
     for (int i = 0; i < 3; ++i) c->occx_nb[i] = (r[i] + 3u) >> 2;
     const uint64_t nb = (uint64_t)c->occx_nb[0] * c->occx_nb[1] * c->occx_nb[2];
@@ -2479,7 +2576,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
                         coarse[cb >> 5] |= 1u << (cb & 31);
                     }
                 }
-        HIP_TRY(hipMemcpy(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice));
+        HIP_TRY(copy_sync(c->d_occ, coarse.data(), 4ull * c->occ_words, hipMemcpyHostToDevice, c->stream));
         if (!occx_possible) {
             c->occx_ok = false;
             const int rc = context_sat(c);
@@ -2508,7 +2605,7 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
             c->occx_nbw = (uint32_t)nbw;
             c->occx_moff = (uint32_t)moff;
             HIP_TRY(hipMalloc((void**)&c->d_occx, words * 4));
-            HIP_TRY(hipMemcpy(c->d_occx, blob.data(), words * 4, hipMemcpyHostToDevice));
+            HIP_TRY(copy_sync(c->d_occx, blob.data(), words * 4, hipMemcpyHostToDevice, c->stream));
         }
     } else if (!occx_possible) {
         HIP_TRY(hipMemsetAsync(c->d_occ, 0, 4ull * c->occ_words, c->stream));
@@ -2572,7 +2669,9 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
     }
     // (the escape table itself is built by the first render whose frame is
     // large enough to pay for it: context_escape)
+    sc_occ.mark(c, "occupancy bits + OccX");
     const int rc = context_sat(c);
+    sc_occ.mark(c, "summed-area table");
     if (rc != ZRT_OK) return rc;
     return context_counters(c);
 }
@@ -2633,12 +2732,15 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
     if (!c) return ZRT_ERR_OUT_OF_MEMORY;
     c->device = device;
     c->mt_exact = mt_exact;
+    StageClock sc;
     rc = context_base(c);
     if (rc == ZRT_OK) {
+        sc.mark(c, "stream + device properties");
         zrt::Grid grid;
         DeviceGeometry dg;
         rc = grid_build_into_device(positions, normals, texcoords, material, num_triangles, resolution, c->stream,
                                     &grid, &dg);
+        if (rc == ZRT_OK) sc.mark(c, "grid build + bake (grid_build.hip)");
         if (rc == ZRT_OK) {
             for (int i = 0; i < 3; ++i) {
                 c->grid.bbox_min[i] = (&grid.bbox.min.x)[i];
@@ -2651,7 +2753,10 @@ extern "C" int zrt_context_create_built(const float* positions, const float* nor
             c->d_cells = dg.cells;
             c->d_data = dg.data;               // the context owns both from here (freed by destroy)
             c->d_pos = reinterpret_cast<float*>(dg.pos);   // the device bake's 3 float4 per ref
-            if (rc == ZRT_OK && (rc = context_materials(c, &ms)) == ZRT_OK) rc = context_occupancy(c, nullptr);
+            if (rc == ZRT_OK && (rc = context_materials(c, &ms)) == ZRT_OK) {
+                sc.mark(c, "materials + texels");
+                rc = context_occupancy(c, nullptr);
+            }
         }
     }
     if (rc != ZRT_OK) { zrt_context_destroy(c); return rc; }
@@ -2753,7 +2858,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         c->pix.resize(n);
         int r2 = grow(&c->d_pix, &c->pix_cap, std::max<size_t>(n, 1));
         if (r2 != ZRT_OK) return r2;
-        if (n) HIP_TRY(hipMemcpy(c->d_pix, c->pix.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        if (n) HIP_TRY(copy_sync(c->d_pix, c->pix.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
         memcpy(c->pix_key, key, sizeof key);
         c->pix_valid = true;
     }
@@ -2896,6 +3001,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                                          : (esc ? (WfFn)wf_park_kernel<true, false> : (WfFn)wf_park_kernel<false, false>))
                                   : mtx ? kWfBounceExact : (packed ? (pbm ? kWfBounceBM : kWfBounce) : kWfBounceWide);
     const WfFn s_next = c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true> : (WfFn)wf_shade_kernel<false>;
+    // a pass's last bounce launch: the terminal-radiance-only shade (LAST)
+    const WfFn s_last = !ZRT_SHADE_LAST ? s_next
+                        : c->nmat <= kLdsMats ? (WfFn)wf_shade_kernel<true, true> : (WfFn)wf_shade_kernel<false, true>;
     const size_t lds_shade = c->nmat <= kLdsMats ? c->nmat * sizeof(DevMat) : 0;
     for (uint32_t k = 0; k < nsets && park_next; ++k)
         if ((rc = grow(&c->set[k].hit, &c->set[k].hit_cap, T)) != ZRT_OK) return rc;
@@ -2953,7 +3061,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         *blocks = (uint32_t)(c->num_cus * bpc);
         return ZRT_OK;
     };
-    uint32_t grid_first = 0, grid_next = 0, grid_count = 0, grid_shade = 0;
+    uint32_t grid_first = 0, grid_next = 0, grid_count = 0, grid_shade = 0, grid_shade_last = 0;
     const int thr_first = kTraceThreads;
     const int thr_next = park_next ? park_block : kTraceThreads;
     const size_t lds_first = lds_wf, lds_next = park_next ? lds_park : lds_wf;
@@ -2963,6 +3071,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         if ((rc = grid_for((const void*)f_first, thr_first, lds_first, &grid_first)) != ZRT_OK) return rc;
         if ((rc = grid_for((const void*)f_next, thr_next, lds_next, &grid_next)) != ZRT_OK) return rc;
         if ((rc = grid_for((const void*)s_next, kTraceThreads, lds_shade, &grid_shade)) != ZRT_OK) return rc;
+        if ((rc = grid_for((const void*)s_last, kTraceThreads, lds_shade, &grid_shade_last)) != ZRT_OK) return rc;
     }
 
     TraceParams tp;
@@ -3128,7 +3237,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 ++kp.launches[cls];
                 if (k > 0 && park_next) {                    // same bounce, shading half
                     if ((rc = kt_begin(ZRT_KERNEL_SHADE, sm)) != ZRT_OK) return rc;
-                    hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), lds_shade, sm, W);
+                    if (k + 1 == nb)
+                        hipLaunchKernelGGL(s_last, dim3(grid_shade_last), dim3(kTraceThreads), lds_shade, sm, W);
+                    else
+                        hipLaunchKernelGGL(s_next, dim3(grid_shade), dim3(kTraceThreads), lds_shade, sm, W);
                     HIP_TRY(hipGetLastError());
                     if ((rc = kt_end(sm)) != ZRT_OK) return rc;
                     ++kp.launches[ZRT_KERNEL_SHADE];
@@ -3175,7 +3287,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     HIP_TRY(hipStreamSynchronize(c->stream));
 
     unsigned long long hs[64];
-    HIP_TRY(hipMemcpy(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost));
+    HIP_TRY(copy_sync(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost, c->stream));
     // diagnostics (debugging only): counting-build walk/test trip counts,
     // per-launch device times
     if (getenv("ZRT_CELL_STATS") && counting)
@@ -3239,12 +3351,12 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         std::vector<uint8_t> tmp;
         uint8_t* dst = outs->rgb_packed;
         if (!dst) { tmp.resize(3ull * P); dst = tmp.data(); }
-        HIP_TRY(hipMemcpy(dst, c->d_rgb, 3ull * P, hipMemcpyDeviceToHost));
+        HIP_TRY(copy_sync(dst, c->d_rgb, 3ull * P, hipMemcpyDeviceToHost, c->stream));
         if (outs->rgb_image)
             for (uint32_t q = 0; q < P; ++q) memcpy(outs->rgb_image + 3ull * c->pix[q], dst + 3ull * q, 3);
     }
     if (want_lin)
-        HIP_TRY(hipMemcpy(outs->linear_packed, c->d_lin, 3ull * P * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_TRY(copy_sync(outs->linear_packed, c->d_lin, 3ull * P * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     if (stats) *stats = st;
     return ZRT_OK;
 }
@@ -3254,6 +3366,8 @@ extern "C" int zrt_context_profile(const zrt_context* c, zrt_kernel_profile* out
     *out = c->prof;
     return ZRT_OK;
 }
+
+void* zrt::context_stream(const zrt_context* c) { return c ? (void*)c->stream : nullptr; }
 
 void zrt::context_set_mem_share(zrt_context* c, uint32_t share) {
     if (c) c->mem_share = std::max<uint32_t>(share, 1u);

@@ -60,4 +60,10 @@ int context_device_rgb(const zrt_context* c, const uint8_t** d_rgb, uint32_t* pi
 // share = how often the device appears in the list).
 void context_set_mem_share(zrt_context* c, uint32_t share);
 
+// The context's main HIP stream (as a void*: this header has no HIP types):
+// a group gathers on its first context's stream instead of creating one of
+// its own (a stream's first hardware queue cost ~10-17 ms of the CLI's
+// start-up, r06d).
+void* context_stream(const zrt_context* c);
+
 }  // namespace zrt
