@@ -332,6 +332,12 @@ enum {
                                  equals NaN), the smallest such bits (0xFFFFFFFF: none), 0, 0};
                                  every float of each range, on the device */
     ZRT_PROBE_TRIANGLE_EXACT = 11, /* as TRIANGLE, with the IEEE division of the ZRT_FLAG_MT_EXACT kernels */
+    ZRT_PROBE_QUOT = 12,      /* in n*2 floats (a, b) -> out n*2: dda_init_fq's quotient quot_rn(a, b,
+                                 1/b by the short reciprocal), the IEEE a / b */
+    ZRT_PROBE_QUOT_SWEEP = 13, /* in n*2 u32 {first significand s_b, count} -> out n*4 u32 {pairs whose
+                                 quot_rn differs in any bit from the IEEE quotient, the first such a's
+                                 bits, its b's bits, 0}: every a in [1, 2) against every
+                                 b = 1 + s / 2^23, s in [s_b, s_b + count), on the device */
 };
 int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device);
 /* Comma-separated substrings of the mangled names of the timed kernel

@@ -321,6 +321,119 @@ def test_probe_bbox_and_dda(oracle_mod, rng):
     assert walked > 100
 
 
+def _quot_pairs(rng):
+    """(a, b) f32 pairs over dda_init_fq's operand range -- numerators 0 or
+    2^-64 .. 2^64, divisors 2^-32 .. 2^32, both signs, seeded significands --
+    plus its edges: +-0 numerators (the copysign), the range's end exponents,
+    all-ones and all-zeros significands."""
+    f32 = np.float32
+    n = 200_000
+    ea = rng.integers(-64, 64, n)
+    eb = rng.integers(-32, 32, n)
+    ma = rng.integers(0, 1 << 23, n, dtype=np.int64)
+    mb = rng.integers(0, 1 << 23, n, dtype=np.int64)
+    a = (((ea + 127).astype(np.uint32) << 23) | ma.astype(np.uint32)).view(f32)
+    b = (((eb + 127).astype(np.uint32) << 23) | mb.astype(np.uint32)).view(f32)
+    a = np.where(rng.random(n) < 0.5, -a, a)
+    b = np.where(rng.random(n) < 0.5, -b, b)
+    edge_a = [0.0, -0.0, 2.0 ** -64, 2.0 ** 64, 1.9999999, 1.0, 3.0, -2.0 ** 64]
+    edge_b = [2.0 ** -32, 2.0 ** 32, 1.9999999, 1.0, -1.0, 0.1, -0.7, 3.0]
+    ea2, eb2 = np.meshgrid(np.array(edge_a, f32), np.array(edge_b, f32))
+    return np.concatenate([a, ea2.ravel()]).astype(f32), np.concatenate([b, eb2.ravel()]).astype(f32)
+
+
+def test_probe_quot_vs_host_division(rng):
+    """dda_init_fq's quotient (zrt_math.h quot_rn: Markstein's correction
+    from the short reciprocal) equals the host's IEEE f32 division bit for
+    bit -- zero signs included -- on 200 K seeded pairs over its operand range
+    and the range's edges (VERDICT r5 #4; linalg.zig:324-349, :443-469)."""
+    a, b = _quot_pairs(rng)
+    n = a.size
+    out = native.probe(native.PROBE_QUOT, np.stack([a, b], 1), n, (n, 2))
+    host = (a / b).astype(np.float32)
+    bad = np.flatnonzero(out[:, 0].view(np.uint32) != host.view(np.uint32))
+    assert bad.size == 0, (a[bad[:5]], b[bad[:5]], out[bad[:5], 0], host[bad[:5]])
+    assert np.array_equal(out[:, 1].view(np.uint32), host.view(np.uint32))
+
+
+def test_probe_quot_sweep_significand_pairs():
+    """Every a significand against 4,096 b significands spread over [1, 2)
+    plus the first and last 64 (2^35 pairs, the device's IEEE division as the
+    reference); tools/quot_sweep.py runs all 2^46 pairs (DESIGN.md 5.5e)."""
+    starts = [(0, 64), ((1 << 23) - 64, 64)] + [(k * 2048 + 977, 1) for k in range(4096)]
+    inp = np.array(starts, np.uint32)
+    out = native.probe(native.PROBE_QUOT_SWEEP, inp, len(starts), (len(starts), 4), np.uint32)
+    bad = np.flatnonzero(out[:, 0])
+    assert bad.size == 0, [(starts[i], hex(out[i, 2]), hex(out[i, 3])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("box", ["unit", "offset", "tiny_cells", "huge", "at_origin"])
+def test_probe_dda_fast_quotient_edge_rays(oracle_mod, rng, box):
+    """The kernels' dda_init (dda_init_fq: quotients where its operand
+    range holds, the IEEE dda_init elsewhere) against the oracle, bit for
+    bit, on rays that reach both branches: origins on the bbox planes and
+    on cell boundaries (zero numerators), 1e-30 off a plane at 0 (a tiny
+    numerator: the fallback), zero / -0 / 1e-12 direction components (the
+    fallback), 1e-9 ones (quotients), cells of 1e-12 (cs outside
+    [2^-32, 2^32]: the whole grid falls back) and coordinates of 1e25."""
+    lo, hi = {"unit": ((0, 0, 0), (5, 3, 4)), "offset": ((-3.5, 1.25, -7), (2.5, 4.0, 1)),
+              "tiny_cells": ((0, 0, 0), (5e-12, 3e-12, 4e-12)), "huge": ((0, 0, 0), (5e25, 3e25, 4e25)),
+              "at_origin": ((0, 0, 0), (1, 1, 1))}[box]
+    lo, hi = np.asarray(lo, np.float64), np.asarray(hi, np.float64)
+    ext = hi - lo
+    res = np.array([5, 7, 3], np.uint32)
+    cases = []
+    for k in range(400):
+        kind = k % 8
+        o = lo + ext * rng.uniform(-0.5, 1.5, 3)
+        tgt = lo + ext * rng.uniform(0, 1, 3)
+        d = tgt - o
+        if kind == 1:                                   # on a bbox plane
+            o[k % 3] = lo[k % 3] if k & 1 else hi[k % 3]
+        elif kind == 2:                                 # on cell boundaries
+            o = lo + ext * rng.integers(0, 6, 3) / np.array([5.0, 7.0, 3.0])
+        elif kind == 3:                                 # a zero / -0 component
+            d[k % 3] = 0.0 if k & 1 else -0.0
+        elif kind == 4:                                 # tiny / small components
+            d[k % 3] = 1e-12 if k & 1 else 1e-9 * max(abs(d).max(), 1e-30)
+        elif kind == 5:                                 # 1e-30 off the plane at the origin box
+            o[k % 3] = lo[k % 3] + (1e-30 if k & 1 else -1e-30)
+        d = np.asarray(d, np.float32)
+        if not np.any(d):
+            d[0] = 1.0
+        dn = _norm(d)
+        if not np.all(np.isfinite(dn)):
+            continue
+        cases.append((lo, hi, np.asarray(o, np.float32), dn))
+    n = len(cases)
+    inp = np.array([list(a) + list(b) + list(c) + list(d) for a, b, c, d in cases], np.float32)
+    outd = native.probe(native.PROBE_DDA, inp, n, (n, native.DDA_PROBE_WIDTH), aux=res)
+    walked = 0
+    for i, (l, h, o, d) in enumerate(cases):
+        tr = oracle_mod.grid_trace(np.float32(l), np.float32(h), tuple(res), o, d, 64)
+        if tr is None:
+            assert outd[i, 0] == -1, i
+            continue
+        first, cells, ts = tr
+        k = int(outd[i, 0])
+        assert k == len(ts), (i, k, len(ts))
+        assert tuple(int(x) for x in outd[i, 1:4]) == tuple(int(x) for x in first), i
+        got = outd[i, 4:4 + 4 * k].reshape(k, 4)
+        # (the probe reports the cell before the step for a +inf crossing,
+        # the exit cell's convention; a +inf crossing off the exit cell --
+        # t overflowing on the 1e25 box -- stops the walk all the same)
+        m = k - 1 if ts[-1] == np.inf else k
+        assert np.array_equal(got[:m, :3].astype(np.uint32), cells[:m]), i
+        # t bit for bit, except the sign of a zero: Zig's @max(0, t)
+        # (linalg.zig:448, llvm.maxnum) may return either zero, and so do the
+        # host's fmaxf and the device's v_max_f32; a zero t is only compared
+        tg, to = got[:, 3].astype(np.float32), ts.astype(np.float32)
+        z = (tg == 0) & (to == 0)
+        assert _same_bits(np.where(z, 0, tg), np.where(z, 0, to)), (i, tg, to)
+        walked += 1
+    assert walked > 100
+
+
 def test_probe_to_rgb_exp_log(oracle_mod, rng):
     vals = np.concatenate([rng.uniform(0, 1.2, (2000, 3)), rng.uniform(0, 1e-3, (500, 3)),
                            np.array([[0, 1, 2], [np.nan, np.inf, -1], [1e-40, 0.999999, 1e30]])])

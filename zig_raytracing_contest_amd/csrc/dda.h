@@ -50,6 +50,84 @@ ZHD bool dda_init(const float* bmin, const float* bmax, const uint32_t* res, con
     return true;
 }
 
+// dda_init with its fifteen f32 divisions (bbox_ray's six, then three cell
+// indices, three t_delta and three first crossings) as quot_rn quotients:
+// one correctly rounded reciprocal of each direction component (the
+// mt_inv_det sequence, exact for normal |d| <= 2^126) shared by the four
+// divisions by it, and the cell sizes' reciprocals RN(1 / cs) from the host
+// (`ics`, valid when `cs_ok`: every cs in [2^-32, 2^32]).  When every
+// numerator is 0 or of magnitude in [2^-64, 2^64] (or NaN) and every |d| in
+// [2^-32, 1], each quotient is the division's bit for bit (quot_rn), so the
+// state is dda_init's; otherwise the lane recomputes it with dda_init.  The
+// check costs ~2 VALU per operand; 11-VALU divisions become 4-VALU quotients
+// (DESIGN 5.5e).
+#ifndef ZRT_FAST_QUOT
+#define ZRT_FAST_QUOT 1
+#endif
+#if defined(__HIPCC__)
+// (bits << 1) - 2 of a float: its magnitude's bits doubled, minus 2 -- zero
+// wraps to the top, so a minimum >= 2 * bits(2^-64) - 2 says "0 or >= 2^-64"
+ZHD uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+__device__ __forceinline__ uint32_t quot_low3(float a, float b, float c) {
+    const uint32_t x = (fbits(a) << 1) - 2u, y = (fbits(b) << 1) - 2u, z = (fbits(c) << 1) - 2u;
+    return zmin(x, zmin(y, z));
+}
+__device__ __forceinline__ float abs_max3(float a, float b, float c) {
+    return fmaxf(fabsf(a), fmaxf(fabsf(b), fabsf(c)));
+}
+__device__ __forceinline__ bool dda_init_fq(const float* bmin, const float* bmax, const uint32_t* res, const float* cs,
+                                            const float* ics, bool cs_ok, v3 o, v3 d, Dda& s) {
+    const float yx = mt_inv_det<false>(d.x), yy = mt_inv_det<false>(d.y), yz = mt_inv_det<false>(d.z);
+    // bbox_ray (linalg.zig:324-349)
+    const bool sx = d.x < 0.0f, sy = d.y < 0.0f, sz = d.z < 0.0f;
+    const float lx = (sx ? bmax[0] : bmin[0]) - o.x, ly = (sy ? bmax[1] : bmin[1]) - o.y,
+                lz = (sz ? bmax[2] : bmin[2]) - o.z;
+    const float hx = (sx ? bmin[0] : bmax[0]) - o.x, hy = (sy ? bmin[1] : bmax[1]) - o.y,
+                hz = (sz ? bmin[2] : bmax[2]) - o.z;
+    const float mnx = quot_rn(lx, d.x, yx), mny = quot_rn(ly, d.y, yy), mnz = quot_rn(lz, d.z, yz);
+    const float mxx = quot_rn(hx, d.x, yx), mxy = quot_rn(hy, d.y, yy), mxz = quot_rn(hz, d.z, yz);
+    float tmin = mnx, tmax = mxx;
+    bool hit = !((tmin > mxy) || (tmax < mny));
+    tmin = fmaxf(tmin, mny);
+    tmax = fminf(tmax, mxy);
+    hit = hit && !((tmin > mxz) || (tmax < mnz));
+    tmin = fmaxf(tmin, mnz);
+    // Grid.traceRay (linalg.zig:443-469)
+    const float t_hit = fmaxf(0.0f, tmin);
+    const v3 local = sub(add(o, scale(d, t_hit)), mk(bmin[0], bmin[1], bmin[2]));
+    const bool n0 = sx, n1 = sy, n2 = sz;
+    const uint32_t c0 = zmin(f2u(quot_rn(local.x, cs[0], ics[0])), res[0] - 1u);
+    const uint32_t c1 = zmin(f2u(quot_rn(local.y, cs[1], ics[1])), res[1] - 1u);
+    const uint32_t c2 = zmin(f2u(quot_rn(local.z, cs[2], ics[2])), res[2] - 1u);
+    const float ax = ((float)(c0 + (n0 ? 0u : 1u))) * cs[0] - local.x;
+    const float ay = ((float)(c1 + (n1 ? 0u : 1u))) * cs[1] - local.y;
+    const float az = ((float)(c2 + (n2 ? 0u : 1u))) * cs[2] - local.z;
+    // the operands' range (quot_rn): numerators 0 or in [2^-64, 2^64] (NaN
+    // passes: it stays NaN either way), |d| in [2^-32, 1]
+    const float big = fmaxf(fmaxf(abs_max3(lx, ly, lz), abs_max3(hx, hy, hz)),
+                            fmaxf(abs_max3(local.x, local.y, local.z), abs_max3(ax, ay, az)));
+    const uint32_t low = zmin(zmin(quot_low3(lx, ly, lz), quot_low3(hx, hy, hz)),
+                              zmin(quot_low3(local.x, local.y, local.z), quot_low3(ax, ay, az)));
+    const float dmin = fminf(fabsf(d.x), fminf(fabsf(d.y), fabsf(d.z)));
+    const bool ok = cs_ok && !(big > 0x1p64f) && low >= 2u * 0x1F800000u - 2u && dmin >= 0x1p-32f;
+    if (!ok) return dda_init(bmin, bmax, res, cs, o, d, s);
+    if (!hit) return false;
+    s.c0 = c0; s.c1 = c1; s.c2 = c2;
+    s.neg = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
+    s.td0 = fabsf(quot_rn(cs[0], d.x, yx));
+    s.td1 = fabsf(quot_rn(cs[1], d.y, yy));
+    s.td2 = fabsf(quot_rn(cs[2], d.z, yz));
+    s.tn0 = t_hit + quot_rn(ax, d.x, yx);
+    s.tn1 = t_hit + quot_rn(ay, d.y, yy);
+    s.tn2 = t_hit + quot_rn(az, d.z, yz);
+    s.lin = (s.c2 * res[1] + s.c1) * res[0] + s.c0;
+    const bool fin = s.tn0 > -kInf && s.tn1 > -kInf && s.tn2 > -kInf && s.td0 == s.td0 && s.td1 == s.td1 &&
+                     s.td2 == s.td2;
+    s.neg |= fin ? 0u : 8u;
+    return true;
+}
+#endif
+
 // Iterator.next (linalg.zig:478-496), branch-free.  map[k] with
 // k = (t0<t1)<<2 | (t0<t2)<<1 | (t1<t2) and map = {2,1,2,1,2,2,0,0} is
 // exactly: axis 0 iff t0<t1 && t0<t2; axis 1 iff !(t0<t1) && t1<t2; else 2

@@ -110,6 +110,11 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
 // +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
 // primary frustum bounds per (1 << ZRT_FRUSTUM_SHIFT)^2 pixel block
+// dda_init_fq (dda.h) in the primary / lane-walk wf_kernel too (the park
+// kernel's refill always takes it when ZRT_FAST_QUOT)
+#ifndef ZRT_FAST_QUOT_WF
+#define ZRT_FAST_QUOT_WF 1
+#endif
 #ifndef ZRT_FRUSTUM_SHIFT
 #define ZRT_FRUSTUM_SHIFT 3
 #endif
@@ -132,6 +137,8 @@ struct TraceParams {
     float bmin[3], bmax[3];
     uint32_t res[3];
     float cs[3];
+    float ics[3];             // RN(1 / cs) (host division), for dda_init_fq
+    uint32_t cs_ok;           // every cs in [2^-32, 2^32]: dda_init_fq may use ics
     const uint2* cells;
     const float* tri_pos;     // kTriFloats per ref (see kTriFloats)
     const float4* tri_data;   // 4 per ref: n0 n1 n2 uv0 uv1 uv2 mat
@@ -297,7 +304,13 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                                            float tau = 0.0f, float tfar = kInf) {
     float nearest = kInf;
     Dda s0;
-    if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) return nearest;
+    // (the counting build and the IEEE-division kernels keep dda_init's
+    // divisions; the timed kernels take dda_init_fq's quotients: same state)
+    if (ZRT_FAST_QUOT && ZRT_FAST_QUOT_WF && !MTX && !STATS) {
+        if (!dda_init_fq(p.bmin, p.bmax, p.res, p.cs, p.ics, p.cs_ok != 0u, o, d, s0)) return nearest;
+    } else if (!dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {
+        return nearest;
+    }
     const uint32_t sh = p.occ_shift;
     const GridK gk = grid_consts(p);
     if constexpr (PACKED) {
@@ -1241,7 +1254,8 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                             W.o[lane] = make_float4(o.x, o.y, o.z, 0.0f);
                             W.d[lane] = make_float4(d.x, d.y, d.z, 0.0f);
                             Dda s0;
-                            if (dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
+                            if (ZRT_FAST_QUOT ? dda_init_fq(p.bmin, p.bmax, p.res, p.cs, p.ics, p.cs_ok != 0u, o, d, s0)
+                                              : dda_init(p.bmin, p.bmax, p.res, p.cs, o, d, s0)) {   // stage3.zig:153-156
                                 ddav_from_t<PK_BM>(s0, gk, pk, s);
                                 if (ESC) {
                                     // (every DMA into this slot from the lane's last
@@ -3081,11 +3095,15 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         tp.bmax[i] = c->grid.bbox_max[i];
         tp.res[i] = c->grid.resolution[i];
         tp.cs[i] = c->grid.cell_size[i];
+        tp.ics[i] = 1.0f / c->grid.cell_size[i];          // IEEE: RN(1 / cs)
         tp.org[i] = cam->origin[i];
         tp.llc[i] = cam->lower_left_corner[i];
         tp.right[i] = cam->right[i];
         tp.up[i] = cam->up[i];
     }
+    tp.cs_ok = 1u;
+    for (int i = 0; i < 3; ++i)
+        if (!(fabsf(tp.cs[i]) >= 0x1p-32f && fabsf(tp.cs[i]) <= 0x1p32f)) tp.cs_ok = 0u;
     tp.cells = c->d_cells;
     tp.pk = c->pk;
     tp.cell32 = c->d_cell32;
@@ -3474,7 +3492,14 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             const float bmin[3] = {bb.min.x, bb.min.y, bb.min.z}, bmax[3] = {bb.max.x, bb.max.y, bb.max.z};
             const float cs[3] = {g.cell_size.x, g.cell_size.y, g.cell_size.z};
             Dda s;
-            if (!dda_init(bmin, bmax, r3, cs, ld3(a + 6), ld3(a + 9), s)) { o[0] = -1.0f; break; }
+            // the park kernel's dda_init (dda_init_fq: the quotients from one
+            // reciprocal per axis where exact, else dda_init)
+            const float ics[3] = {1.0f / cs[0], 1.0f / cs[1], 1.0f / cs[2]};
+            bool cs_ok = true;
+            for (int k = 0; k < 3; ++k) cs_ok = cs_ok && fabsf(cs[k]) >= 0x1p-32f && fabsf(cs[k]) <= 0x1p32f;
+            const bool in = ZRT_FAST_QUOT ? dda_init_fq(bmin, bmax, r3, cs, ics, cs_ok, ld3(a + 6), ld3(a + 9), s)
+                                          : dda_init(bmin, bmax, r3, cs, ld3(a + 6), ld3(a + 9), s);
+            if (!in) { o[0] = -1.0f; break; }
             GridK gk;
             gk.rm0 = r3[0] - 1u; gk.rm1 = r3[1] - 1u; gk.rm2 = r3[2] - 1u;
             gk.str1 = r3[0]; gk.str2 = r3[0] * r3[1];
@@ -3541,6 +3566,13 @@ __global__ void probe_kernel(int which, const void* in, void* out, uint32_t n, c
             }
             break;
         }
+        case ZRT_PROBE_QUOT: {
+            const float* a = (const float*)in + 2ull * i;
+            float* o = (float*)out + 2ull * i;
+            o[0] = quot_rn(a[0], a[1], mt_inv_det<false>(a[1]));
+            o[1] = a[0] / a[1];
+            break;
+        }
         case ZRT_PROBE_RECIP: {
             const float x = ((const float*)in)[i];
             float* o = (float*)out + 2ull * i;
@@ -3573,6 +3605,33 @@ __global__ __launch_bounds__(kBlock) void recip_sweep_kernel(uint32_t lo, uint32
     }
 }
 
+// ZRT_PROBE_QUOT_SWEEP: every significand pair (a in [1, 2), b = 1 + s /
+// 2^23 for s in [s0, s0 + ns)), quot_rn against the IEEE division, bit for bit.
+__global__ __launch_bounds__(kBlock) void quot_sweep_kernel(uint32_t s0, uint32_t ns, uint32_t* out) {
+    const uint64_t total = (uint64_t)ns << 23;
+    uint32_t bad = 0;
+    unsigned long long first = ~0ull;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t ab = 0x3F800000u | (uint32_t)(k & 0x7FFFFFu);
+        const uint32_t bb = 0x3F800000u | (s0 + (uint32_t)(k >> 23));
+        const float a = __uint_as_float(ab), b = __uint_as_float(bb);
+        const float q = quot_rn(a, b, mt_inv_det<false>(b));
+        if (__float_as_uint(q) != __float_as_uint(a / b)) {
+            ++bad;
+            first = min(first, ((unsigned long long)bb << 32) | ab);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        bad += __shfl_xor(bad, o);
+        const unsigned lo = __shfl_xor((unsigned)first, o), hi = __shfl_xor((unsigned)(first >> 32), o);
+        first = min(first, ((unsigned long long)hi << 32) | lo);
+    }
+    if ((threadIdx.x & 63u) == 0 && bad) {
+        atomicAdd(&out[0], bad);
+        atomicMin(reinterpret_cast<unsigned long long*>(out + 2), first);
+    }
+}
+
 }  // namespace
 
 extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const void* aux, int device) {
@@ -3590,6 +3649,8 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
         case ZRT_PROBE_EXP_LOG: in_sz = 8; out_sz = 16; break;
         case ZRT_PROBE_RECIP: in_sz = 4; out_sz = 8; break;
         case ZRT_PROBE_RECIP_SWEEP: in_sz = 8; out_sz = 16; break;
+        case ZRT_PROBE_QUOT: in_sz = 8; out_sz = 8; break;
+        case ZRT_PROBE_QUOT_SWEEP: in_sz = 8; out_sz = 16; break;
         case ZRT_PROBE_TEXTURE: {
             in_sz = 8; out_sz = 12;
             if (!aux) return ZRT_ERR_INVALID_ARG;
@@ -3625,7 +3686,20 @@ extern "C" int zrt_probe(int which, const void* in, void* out, uint32_t n, const
             HIP_TRY(hipMalloc(&d_aux, aux_sz));
             HIP_TRY(hipMemcpy(d_aux, aux, aux_sz, hipMemcpyHostToDevice));
         }
-        if (which == ZRT_PROBE_RECIP_SWEEP) {
+        if (which == ZRT_PROBE_QUOT_SWEEP) {
+            // out per range: {mismatches, 0, first (a bits, b bits) as a u64 min}
+            const uint32_t* r = (const uint32_t*)in;
+            std::vector<uint32_t> init(4ull * n, 0u);
+            for (uint32_t k = 0; k < n; ++k) init[4ull * k + 2] = init[4ull * k + 3] = 0xFFFFFFFFu;
+            HIP_TRY(hipMemcpy(d_out, init.data(), out_sz * n, hipMemcpyHostToDevice));
+            for (uint32_t k = 0; k < n; ++k) {
+                if (r[2 * k + 1] == 0) continue;
+                if ((uint64_t)r[2 * k] + r[2 * k + 1] > (1ull << 23)) return ZRT_ERR_INVALID_ARG;
+                hipLaunchKernelGGL(quot_sweep_kernel, dim3(16384), dim3(kBlock), 0, 0, r[2 * k], r[2 * k + 1],
+                                   (uint32_t*)d_out + 4ull * k);
+                HIP_TRY(hipGetLastError());
+            }
+        } else if (which == ZRT_PROBE_RECIP_SWEEP) {
             const uint32_t* r = (const uint32_t*)in;
             std::vector<uint32_t> init(4ull * n, 0u);
             for (uint32_t k = 0; k < n; ++k) init[4ull * k + 1] = 0xFFFFFFFFu;

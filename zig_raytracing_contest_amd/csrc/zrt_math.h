@@ -320,6 +320,20 @@ ZHD float mt_inv_det(float det) {
 #endif
     return 1.0f / det;
 }
+// a / b, correctly rounded, from y = RN(1 / b): Markstein's correction
+// q0 = a y, r = a - b q0 (exact, one fma), q = q0 + r y.  The IEEE quotient bit
+// for bit when b and a / b are normal and r is representable: checked on the
+// device for every pair of significands (a, b in [1, 2):
+// ZRT_PROBE_QUOT_SWEEP), which extends by exact power-of-two scaling to
+// 2^-64 <= |a| <= 2^64 and 2^-32 <= |b| <= 2^32 (quot_operands_ok; the
+// remainder stays exact down there), and a = +-0 (q0 is the signed zero the
+// division gives, the copysign keeps it: r y may add a zero of the other
+// sign).  NaN operands give NaN either way.
+ZHD float quot_rn(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = fmaf(-b, q0, a);
+    return copysignf(fmaf(r, y, q0), q0);
+}
 template <bool IEEE = false>
 ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);

@@ -31,6 +31,7 @@ PROBE_TRIANGLE, PROBE_BBOX, PROBE_DDA, PROBE_TO_RGB = 0, 1, 2, 3
 PROBE_RNG_F32, PROBE_RNG_NORM, PROBE_EXP_LOG, PROBE_TEXTURE = 4, 5, 6, 7
 PROBE_TRIANGLE_FLAT = 8
 PROBE_RECIP, PROBE_RECIP_SWEEP, PROBE_TRIANGLE_EXACT = 9, 10, 11
+PROBE_QUOT, PROBE_QUOT_SWEEP = 12, 13
 DDA_PROBE_WIDTH = 4 + 4 * 64      # floats per ray: steps, first cell, 64 x (cell, t)
 
 
@@ -441,7 +442,8 @@ def timed_kernels():
 _PROBE_IO = {PROBE_TRIANGLE: (60, 16), PROBE_TRIANGLE_FLAT: (60, 16), PROBE_BBOX: (48, 8),
              PROBE_DDA: (48, 4 * DDA_PROBE_WIDTH), PROBE_TO_RGB: (12, 12), PROBE_RNG_F32: (12, 64),
              PROBE_RNG_NORM: (12, 64), PROBE_EXP_LOG: (8, 16), PROBE_TEXTURE: (8, 12),
-             PROBE_RECIP: (4, 8), PROBE_RECIP_SWEEP: (8, 16), PROBE_TRIANGLE_EXACT: (60, 16)}
+             PROBE_RECIP: (4, 8), PROBE_RECIP_SWEEP: (8, 16), PROBE_TRIANGLE_EXACT: (60, 16),
+             PROBE_QUOT: (8, 8), PROBE_QUOT_SWEEP: (8, 16)}
 
 
 def probe(which, inp: np.ndarray, n: int, out_shape, out_dtype=np.float32, aux=None, device=-1):
