@@ -110,6 +110,16 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
 // +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
 // primary frustum bounds per (1 << ZRT_FRUSTUM_SHIFT)^2 pixel block
+// the timed kernels' normalize: 1/length by recip_rn (zrt_math.h; the same
+// vector bit for bit)
+#ifndef ZRT_NORMALIZE_RN
+#define ZRT_NORMALIZE_RN 1
+#endif
+#if ZRT_NORMALIZE_RN
+#define ZRT_NORM_RN normalize_rn
+#else
+#define ZRT_NORM_RN normalize
+#endif
 // dda_init_fq (dda.h) in the primary / lane-walk wf_kernel too (the park
 // kernel's refill always takes it when ZRT_FAST_QUOT)
 #ifndef ZRT_FAST_QUOT_WF
@@ -451,7 +461,7 @@ __device__ __forceinline__ void camera_ray(const TraceParams& p, uint32_t item, 
     const float jx = rng_float(rng);
     const float jy = rng_float(rng);
     o = mk(p.org[0], p.org[1], p.org[2]);
-    d = normalize(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
+    d = ZRT_NORM_RN(add(add(mk(p.llc[0], p.llc[1], p.llc[2]),
                           scale(mk(p.right[0], p.right[1], p.right[2]), (float)px + jx)),
                       scale(mk(p.up[0], p.up[1], p.up[2]), (float)py + jy)));
 }
@@ -725,7 +735,7 @@ __device__ __forceinline__ bool shade_segment(const WfParams& w, const double* z
         const float nx = (float)rng_norm64(rng, zx, zf);
         const float ny = (float)rng_norm64(rng, zx, zf);
         const float nz = (float)rng_norm64(rng, zx, zf);
-        d = normalize(add(nrm, normalize(mk(nx, ny, nz))));
+        d = ZRT_NORM_RN(add(nrm, ZRT_NORM_RN(mk(nx, ny, nz))));
         mask |= 1u << slot;
         SHADE_STAMP(5, d.x);                                // pair store + ziggurat draws
     }

@@ -334,6 +334,21 @@ ZHD float quot_rn(float a, float b, float y) {
     const float r = fmaf(-b, q0, a);
     return copysignf(fmaf(r, y, q0), q0);
 }
+// 1.0f / x, correctly rounded, for every x: the short reciprocal (equal to
+// the division for every normal |x| <= 2^126, the r06b sweep), the division
+// itself for zero, subnormal, larger, infinite or NaN x (a branch that a
+// normalize of a ray direction never takes).
+ZHD float recip_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && ZRT_MT_RCP
+    float r = mt_inv_det<false>(x);
+    if (__builtin_expect(!(fabsf(x) >= 0x1p-126f && fabsf(x) <= 0x1p126f), 0)) r = 1.0f / x;
+    return r;
+#else
+    return 1.0f / x;
+#endif
+}
+// normalize (linalg.zig:123) with recip_rn: the same vector bit for bit
+ZHD v3 normalize_rn(v3 a) { return scale(a, recip_rn(length(a))); }
 template <bool IEEE = false>
 ZHD bool tri_ray(v3 v0, v3 e1, v3 e2, v3 o, v3 d, float* t, float* uu, float* vv) {
     const v3 pvec = cross(d, e2);
