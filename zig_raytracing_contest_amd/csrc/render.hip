@@ -31,9 +31,6 @@
 
 #include "zrt_internal.h"
 #include "dda.h"
-#ifdef ZRT_OSORT_EXP
-#include <hipcub/hipcub.hpp>
-#endif
 #include "escape.h"
 #include "device_geometry.h"
 
@@ -1871,62 +1868,6 @@ TraceFn count_fn(uint32_t max_bounce) {
     return nullptr;
 }
 
-#ifdef ZRT_OSORT_EXP
-// Experiment (not a product path): before a bounce launch,
-// the continuing paths of every XCD region ordered by the Morton code of
-// their origin in the grid (10 bits per axis), so a park wave's rays and the
-// waves running beside it on one XCD start in one small part of the scene:
-// the locality XCD-spatial routing would give, at its strongest.  Keys:
-// region << 30 | morton, empty slots 0xFFFFFFFF; then a gather back into the
-// regions in key order.
-__device__ __forceinline__ uint32_t spread10(uint32_t x) {
-    x &= 0x3FFu;
-    x = (x | (x << 16)) & 0x030000FFu;
-    x = (x | (x << 8)) & 0x0300F00Fu;
-    x = (x | (x << 4)) & 0x030C30C3u;
-    x = (x | (x << 2)) & 0x09249249u;
-    return x;
-}
-__global__ __launch_bounds__(kBlock) void osort_keys_kernel(const float4* __restrict__ q, const uint32_t* n8,
-                                                            const uint32_t* base8, uint32_t T, TraceParams p,
-                                                            unsigned long long* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= T) return;
-    unsigned long long key = ~0ull;
-    for (uint32_t g = 0; g < 8u; ++g) {
-        if (i >= base8[g] && i < base8[g] + n8[g * 32u]) {
-            const float4 o = q[3ull * i];
-            uint32_t c[3];
-            for (int a = 0; a < 3; ++a) {
-                const float f = ((&o.x)[a] - p.bmin[a]) / (p.bmax[a] - p.bmin[a]) * 1024.0f;
-                c[a] = (uint32_t)fminf(fmaxf(f, 0.0f), 1023.0f);
-            }
-            key = ((unsigned long long)g << 30) | spread10(c[0]) | (spread10(c[1]) << 1) | (spread10(c[2]) << 2);
-        }
-    }
-    keys[i] = key;
-    vals[i] = i;
-}
-__global__ __launch_bounds__(kBlock) void osort_gather_kernel(const float4* __restrict__ q,
-                                                              const unsigned long long* keys, const uint32_t* vals,
-                                                              const uint32_t* base8, uint32_t T,
-                                                              float4* __restrict__ out) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= T || keys[i] == ~0ull) return;
-    const uint32_t g = (uint32_t)(keys[i] >> 30);
-    uint32_t lo = 0, hi = i;                     // the region's first sorted index
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((uint32_t)(keys[mid] >> 30) < g) lo = mid + 1; else hi = mid;
-    }
-    const uint64_t dst = base8[g] + (i - lo), src = vals[i];
-    out[3 * dst] = q[3 * src];
-    out[3 * dst + 1] = q[3 * src + 1];
-    out[3 * dst + 2] = q[3 * src + 2];
-}
-#endif
-
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -3331,46 +3272,6 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                     HIP_TRY(hipGetLastError());
                     if ((rc = kt_end(sm)) != ZRT_OK) return rc;
                     ++kp.launches[ZRT_KERNEL_SHADE];
-#ifdef ZRT_OSORT_EXP
-                    if (k + 1 < nb && k + 1 >= (uint32_t)atoi(getenv("ZRT_OSORT_FROM") ? getenv("ZRT_OSORT_FROM") : "2") &&
-                        getenv("ZRT_OSORT")) {
-                        uint32_t hb[8];
-                        for (uint32_t g = 0; g < 8u; ++g) {
-                            const uint32_t nbk = (P + 63u) >> 6;
-                            hb[g] = S * std::min<uint32_t>(P, (nbk * g / 8u) * 64u);
-                        }
-                        static unsigned long long *d_keys = nullptr, *d_k2 = nullptr;
-                        static uint32_t *d_vals = nullptr, *d_v2 = nullptr, *d_b8 = nullptr;
-                        static float4* d_tmp = nullptr;
-                        static void* d_cub = nullptr;
-                        static size_t cap = 0, cub_bytes = 0;
-                        if (cap < T) {
-                            for (void* x : {(void*)d_keys, (void*)d_vals, (void*)d_k2, (void*)d_v2, (void*)d_tmp, d_cub})
-                                if (x) (void)hipFree(x);
-                            HIP_TRY(hipMalloc((void**)&d_keys, 8 * T));
-                            HIP_TRY(hipMalloc((void**)&d_k2, 8 * T));
-                            HIP_TRY(hipMalloc((void**)&d_vals, 4 * T));
-                            HIP_TRY(hipMalloc((void**)&d_v2, 4 * T));
-                            HIP_TRY(hipMalloc((void**)&d_tmp, 48 * T));
-                            if (!d_b8) HIP_TRY(hipMalloc((void**)&d_b8, 64));
-                            cub_bytes = 0;
-                            HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, d_keys, d_k2, d_vals, d_v2,
-                                                                       (int)T, 0, 64, sm));
-                            HIP_TRY(hipMalloc(&d_cub, cub_bytes));
-                            cap = T;
-                        }
-                        HIP_TRY(hipMemcpyAsync(d_b8, hb, 32, hipMemcpyHostToDevice, sm));
-                        hipLaunchKernelGGL(osort_keys_kernel, dim3((uint32_t)((T + kBlock - 1) / kBlock)), dim3(kBlock),
-                                           0, sm, W.q_out, W.n_out8, d_b8, (uint32_t)T, tp, d_keys, d_vals);
-                        size_t tb = cub_bytes;
-                        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(d_cub, tb, d_keys, d_k2, d_vals, d_v2, (int)T, 0, 64,
-                                                                   sm));
-                        hipLaunchKernelGGL(osort_gather_kernel, dim3((uint32_t)((T + kBlock - 1) / kBlock)),
-                                           dim3(kBlock), 0, sm, W.q_out, d_k2, d_v2, d_b8, (uint32_t)T, d_tmp);
-                        HIP_TRY(hipMemcpyAsync(W.q_out, d_tmp, 48ull * T, hipMemcpyDeviceToDevice, sm));
-                        HIP_TRY(hipGetLastError());
-                    }
-#endif
                 }
                 HIP_TRY(hipEventRecord(c->ev_trace[ne++], sm));
                 ++launches;
