@@ -139,6 +139,11 @@ typedef struct zrt_render_config {
                                         an edge component of 2^62 or more or infinite (the other kernels'
                                         short reciprocal of the determinant holds for |det| < 2^126);
                                         same image */
+#define ZRT_FLAG_RELEASE      0x800u /* the park kernel always skips test rounds with too few parked lanes
+                                        that have refs to test (by default only on scenes where enough
+                                        entry faces of the occupied cells have nothing left to test); same
+                                        image */
+#define ZRT_FLAG_NO_RELEASE   0x1000u /* never (wins over ZRT_FLAG_RELEASE); same image */
 
 /* Per-call statistics.  segments = Scene.traceRay calls (primary + bounce +
  * transparency pass-through); Mrays/s = segments / render time. */

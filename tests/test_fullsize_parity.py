@@ -188,9 +188,9 @@ def test_cfg4_on_a_repeated_device_group_whole_frame():
 MODES = {"escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
          "no_frustum": native.FLAG_NO_FRUSTUM, "one_set": native.FLAG_ONE_SET,
          "lane_walk": native.FLAG_LANE_WALK, "mt_exact": native.FLAG_MT_EXACT,
-         "frustum": native.FLAG_FRUSTUM}
+         "frustum": native.FLAG_FRUSTUM, "release": native.FLAG_RELEASE, "no_release": native.FLAG_NO_RELEASE}
 MODE_FRAMES = [(c, m) for c in ("cfg1", "cfg2", "cfg3") for m in MODES if not (c != "cfg1" and m == "frustum")] + \
-    [("cfg5", "escape"), ("cfg5", "no_frustum"), ("cfg5", "lane_walk"), ("cfg5", "mt_exact")]
+    [("cfg5", "escape"), ("cfg5", "no_frustum"), ("cfg5", "lane_walk"), ("cfg5", "mt_exact"), ("cfg5", "release")]
 
 
 @pytest.fixture(scope="module")

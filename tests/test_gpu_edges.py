@@ -111,9 +111,11 @@ _ORACLE = {}
 # bounds forced on (small frames skip them by default): every one of them on
 # every degenerate grid (flat, 1x1x1, 3x5x2, coarse bricks, wide axes, sky)
 # ... and (round 6) the IEEE-division lane walk that scenes with edges of
-# 2^62 or more take (ZRT_FLAG_MT_EXACT forces it on any scene)
+# 2^62 or more take (ZRT_FLAG_MT_EXACT forces it on any scene), and the park
+# release forced on / off
 MODES = {"default": 0, "escape": native.FLAG_ESCAPE, "no_escape": native.FLAG_NO_ESCAPE,
-         "frustum": native.FLAG_FRUSTUM, "mt_exact": native.FLAG_MT_EXACT}
+         "frustum": native.FLAG_FRUSTUM, "mt_exact": native.FLAG_MT_EXACT,
+         "release": native.FLAG_RELEASE, "no_release": native.FLAG_NO_RELEASE}
 
 
 @pytest.mark.parametrize("mode", list(MODES))

@@ -622,6 +622,7 @@ struct WfParams {
     uint32_t occx_ldsw;       // u32 words OccX takes in LDS (multiple of 4): entries + masks
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
+    uint32_t rel_min;         // park release: a round with fewer parked lanes with refs is skipped (0: off)
     // escape table (escape.h): kEscWords u32 per 4^3 brick, bit b of word
     // w = direction bin 32 w + b; null: not built (the walk never stops early)
     const uint32_t* esc;
@@ -1034,6 +1035,16 @@ constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 #ifndef ZRT_PARK_ADAPT
 #define ZRT_PARK_ADAPT 1
 #endif
+// Park release (round 6): a parked lane whose cell has no ref left to test
+// for the face it entered across (the entry-face mask is 0: every ref was
+// tested in the cell it left) costs a test round nothing but its latency,
+// and 54% of the parks on cfg3 are such (r06n).  Once a round's ranges have
+// landed, a round with fewer than `rel_min` parked lanes that have refs to
+// test is not run while lanes still walk: the empty ones walk on (what the
+// round would have done with them), the others stay parked for the next
+// round.  The context turns it on for scenes where enough of the occupied
+// cells' entry faces have empty masks (context_release; ZRT_FLAG_RELEASE /
+// ZRT_FLAG_NO_RELEASE force it): images identical either way.
 //
 // Issued by inline asm, not the builtin: the compiler treats an LDS-DMA like
 // a store whose VGPR operands are read late, so whenever the register
@@ -1126,7 +1137,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[20] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -1181,7 +1192,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
-    const uint32_t test_min = w.test_min, refill_min = w.refill_min;
+    const uint32_t test_min = w.test_min, refill_min = w.refill_min, rel_min = w.rel_min;
     const GridK gk = grid_consts(p);
     constexpr uint32_t kIdle = 0, kWalk = 1, kPark = 2, kDone = 3;
     uint32_t st = kIdle;
@@ -1424,6 +1435,14 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
             const uint32_t rb = rng_slot[lane], re = rng_slot[64 + lane], cnt = re - rb;
             const uint32_t keep = cnt < 32u ? rng_slot[128 + lane] & ((1u << cnt) - 1u) : rng_slot[128 + lane];
             const uint32_t n = ready ? (cnt <= 32u ? (uint32_t)__popc(keep) : cnt) : 0u;
+            // park release (above): a round with fewer than rel_min parked
+            // lanes that have refs to test is not run while lanes walk
+            if (rel_min != 0u && __ballot(st == kWalk) != 0ull &&
+                (uint32_t)__popcll(__ballot(ready && n != 0u)) < rel_min) {
+                PARK_COUNT(19, __popcll(__ballot(ready && n == 0u)));
+                if (ready && n == 0u) st = kWalk;
+                continue;
+            }
             uint32_t tot = 0;
             const uint32_t off = wave_excl_sum(n, lane, tot);
             PARK_COUNT(5, 1);
@@ -1486,7 +1505,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
     if (lane == 0)
-        for (int k = 13; k < 19; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
+        for (int k = 13; k < 20; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
 #endif
 }
 
@@ -1938,6 +1957,10 @@ struct zrt_context {
     // the primary frustum bounds (frustum_kernel) per 8x8 pixel block
     float4* d_tlo = nullptr; size_t tlo_cap = 0;
     bool esc_on = false;            // the park launches use it (dense enough to pay, context_escape)
+    // park release (wf_park_kernel): the fraction of the occupied cells'
+    // entry-face masks that are 0, and whether the launches use it
+    double rel_frac = 0.0;
+    bool rel_on = false;
     bool esc_tried = false;         // context_escape ran (at the first render that can use it)
     double esc_density = 0.0;       // fraction of its (brick, bin) bits set
     uint32_t occx_words = 0, occx_nbw = 0, occx_moff = 0, occx_nb[3] = {0, 0, 0};
@@ -2278,10 +2301,32 @@ __global__ __launch_bounds__(kBlock) void cell32_kernel(const uint2* __restrict_
     }
 }
 
+// Park release statistic (context_release): over the occupied cells of the
+// packed records, how many (cell, entry face) masks are 0 -- out[0] masks
+// of occupied cells, out[1] zero masks among them.
+__global__ __launch_bounds__(kBlock) void release_stat_kernel(const uint32_t* __restrict__ rec, uint64_t n,
+                                                              unsigned long long* __restrict__ out) {
+    unsigned long long faces = 0, zero = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t* r = rec + 8 * i;
+        if (r[1] > r[0]) {
+            faces += 6;
+            for (int f = 0; f < 6; ++f) zero += r[2 + f] == 0u ? 1 : 0;
+        }
+    }
+    faces = wave_sum(faces);
+    zero = wave_sum(zero);
+    if ((threadIdx.x & 63u) == 0) {
+        atomicAdd(&out[0], faces);
+        atomicAdd(&out[1], zero);
+    }
+}
+
 // The packed walks' layout (DdaV) and their cell records (cell32_kernel;
 // none beyond 16 GiB, or beyond 1 GiB and 16x the cells' own 8 B -- flat
 // grids whose narrow axis pack_layout widened: such a grid walks unpacked).
 constexpr uint64_t kCell32Max = 16ull << 30;
+constexpr double kRelMinFrac = 0.25;   // park release from this fraction of empty entry-face masks
 static int context_packed(zrt_context* c) {
     const uint32_t* r = c->grid.resolution;
     // brick-major words where the grid allows them and the primary's
@@ -2299,6 +2344,28 @@ static int context_packed(zrt_context* c) {
                        0, c->stream, c->d_cells, r[0], r[1], r[2], c->ncells, c->pk, c->d_pos,
                        c->d_cell32);
     HIP_TRY(hipGetLastError());
+    // the park release pays on scenes whose rays often park in a cell with
+    // nothing left to test for their entry face: r06q/r06r, alternating
+    // processes, images identical: Cornell box (65% of the occupied cells'
+    // entry faces empty) +7%, contest stand-in (29%) +3%, Sponza-scale
+    // stand-in (18%) -1.5% (profiles/r06/r06q_ab_park_release.log)
+    {
+        unsigned long long h[2] = {0, 0};
+        unsigned long long* d = nullptr;
+        HIP_TRY(hipMalloc((void**)&d, sizeof h));
+        hipError_t e = hipMemsetAsync(d, 0, sizeof h, c->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(release_stat_kernel, dim3(std::min<uint64_t>((n + kBlock - 1) / kBlock, 4096)),
+                               dim3(kBlock), 0, c->stream, (const uint32_t*)c->d_cell32, n, d);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(d);
+        HIP_TRY(e);
+        c->rel_frac = h[0] ? (double)h[1] / (double)h[0] : 0.0;
+        c->rel_on = c->rel_frac >= kRelMinFrac;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return ZRT_OK;
 }
@@ -3003,6 +3070,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK) &&
                            c->packed && !mtx;
     uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
+    // the park release (wf_park_kernel): where enough entry faces are empty
+    // (context_packed), or as the flags force it (same image either way)
+    const bool rel = !(cfg->flags & ZRT_FLAG_NO_RELEASE) && (c->rel_on || (cfg->flags & ZRT_FLAG_RELEASE));
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
@@ -3073,8 +3143,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const uint32_t occx_ldsw = (uint32_t)occx_lds_words(c->occx_nbw, c->occx_moff, c->occx_words);
     const size_t lds_park = 4ull * occx_ldsw + (size_t)(park_block / 64) * sizeof(ParkSlot);
     if (getenv("ZRT_WF_DEBUG"))
-        fprintf(stderr, "{\"zrt_park_lds\": {\"occx_bytes\": %u, \"block\": %d, \"lds_per_block\": %zu}}\n",
-                4u * occx_ldsw, park_block, lds_park);
+        fprintf(stderr, "{\"zrt_park_lds\": {\"occx_bytes\": %u, \"block\": %d, \"lds_per_block\": %zu, "
+                "\"release_frac\": %.4f, \"release\": %d}}\n",
+                4u * occx_ldsw, park_block, lds_park, c->rel_frac, rel ? 1 : 0);
     auto grid_for = [&](const void* f, int threads, size_t lds, uint32_t* blocks) -> int {
         int bpc = 0;
         HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -3244,6 +3315,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.occx_nb01 = c->occx_nb[0] * c->occx_nb[1];
             W.test_min = test_min;
             W.refill_min = refill_min;
+            W.rel_min = rel ? test_min : 0u;
             W.esc = c->d_esc;
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? q0 : q1;
@@ -3336,8 +3408,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
                 hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23], hs[24], hs[25], hs[26], hs[27], hs[28]);
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_walk_steps\": {\"lane_steps\": %llu, \"empty_brick_steps\": %llu, "
-                "\"empty_brick_entries\": %llu, \"escapes\": %llu, \"parked_tested\": %llu, \"parked_no_refs\": %llu}}\n",
-                hs[48], hs[49], hs[50], hs[51], hs[52], hs[53]);
+                "\"empty_brick_entries\": %llu, \"escapes\": %llu, \"parked_tested\": %llu, \"parked_no_refs\": %llu, "
+                "\"released_early\": %llu}}\n",
+                hs[48], hs[49], hs[50], hs[51], hs[52], hs[53], hs[54]);
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);

@@ -24,6 +24,7 @@ FLAG_ESCAPE, FLAG_NO_ESCAPE = 0x40, 0x80
 FLAG_FRUSTUM, FLAG_NO_FRUSTUM = 0x100, 0x200
 FLAG_ONE_SET, FLAG_KERNEL_TIMES = 0x10, 0x20
 FLAG_MT_EXACT = 0x400
+FLAG_RELEASE, FLAG_NO_RELEASE = 0x800, 0x1000
 # zrt_kernel_profile classes (include/zrt.h)
 KERNEL_CLASSES = ("primary", "park", "shade", "bounce", "resolve", "count")
 
