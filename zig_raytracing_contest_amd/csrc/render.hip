@@ -1864,6 +1864,10 @@ constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
 #define ZRT_PARK_R 20
 #endif
 constexpr uint32_t kParkTestMin = ZRT_PARK_T;
+#ifndef ZRT_PARK_T_REL
+#define ZRT_PARK_T_REL 12
+#endif
+constexpr uint32_t kParkTestMinRel = ZRT_PARK_T_REL;   // with the park release
 constexpr uint32_t kParkRefillMin = ZRT_PARK_R;
 // packed walk state when every axis has at most kPackMaxRes cells
 const WfFn kWfPrimary = (WfFn)wf_kernel<kWfMinWaves0, true, true>;
@@ -3069,13 +3073,21 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     const bool mtx = c->mt_exact || (cfg->flags & ZRT_FLAG_MT_EXACT);
     const bool park_next = c->occx_ok && !counting && !(cfg->flags & ZRT_FLAG_LANE_WALK) &&
                            c->packed && !mtx;
-    uint32_t test_min = kParkTestMin, refill_min = kParkRefillMin;
     // the park release (wf_park_kernel): where enough entry faces are empty
-    // (context_packed), or as the flags force it (same image either way)
+    // (context_packed), or as the flags force it (same image either way);
+    // with it the test rounds start at 12 parked lanes instead of 14 (r06u,
+    // in one process, images identical: cfg3 7004 vs 6979, cfg2 4795 vs
+    // 4632 Mrays/s; 10: 6987 / 4815, 8: 6927 / 4748;
+    // profiles/r06/r06u_knobs_release_trigger.log)
     const bool rel = !(cfg->flags & ZRT_FLAG_NO_RELEASE) && (c->rel_on || (cfg->flags & ZRT_FLAG_RELEASE));
+    uint32_t test_min = rel ? kParkTestMinRel : kParkTestMin, refill_min = kParkRefillMin;
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_T")) test_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
+#endif
+    uint32_t rel_min = test_min;           // park release: the parked lanes with refs a round needs
+#if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
+    if (const char* e = getenv("ZRT_PARK_REL")) rel_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     const bool packed = c->packed && !mtx;
     const bool pbm = packed && c->pk.bm;   // brick-major packed words (dda.h)
@@ -3315,7 +3327,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.occx_nb01 = c->occx_nb[0] * c->occx_nb[1];
             W.test_min = test_min;
             W.refill_min = refill_min;
-            W.rel_min = rel ? test_min : 0u;
+            W.rel_min = rel ? rel_min : 0u;
             W.esc = c->d_esc;
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? q0 : q1;
