@@ -623,6 +623,7 @@ struct WfParams {
     uint32_t test_min;        // parked lanes before a wave runs a test round
     uint32_t refill_min;      // finished lanes before a wave shades and refills
     uint32_t rel_min;         // park release: a round with fewer parked lanes with refs is skipped (0: off)
+    uint32_t rel_emin;        //   ... if at least this many parked lanes have none
     // escape table (escape.h): kEscWords u32 per 4^3 brick, bit b of word
     // w = direction bin 32 w + b; null: not built (the walk never stops early)
     const uint32_t* esc;
@@ -1438,7 +1439,8 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
             // park release (above): a round with fewer than rel_min parked
             // lanes that have refs to test is not run while lanes walk
             if (rel_min != 0u && __ballot(st == kWalk) != 0ull &&
-                (uint32_t)__popcll(__ballot(ready && n != 0u)) < rel_min) {
+                (uint32_t)__popcll(__ballot(ready && n != 0u)) < rel_min &&
+                (uint32_t)__popcll(__ballot(ready && n == 0u)) >= w.rel_emin) {
                 PARK_COUNT(19, __popcll(__ballot(ready && n == 0u)));
                 if (ready && n == 0u) st = kWalk;
                 continue;
@@ -3086,8 +3088,10 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (const char* e = getenv("ZRT_PARK_R")) refill_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     uint32_t rel_min = test_min;           // park release: the parked lanes with refs a round needs
+    uint32_t rel_emin = 1;                 //   and the empty ones that make skipping it worth it
 #if defined(ZRT_SWEEP) || defined(ZRT_SETS_ENV)
     if (const char* e = getenv("ZRT_PARK_REL")) rel_min = (uint32_t)std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("ZRT_PARK_REL_E")) rel_emin = (uint32_t)std::max(1, std::min(64, atoi(e)));
 #endif
     const bool packed = c->packed && !mtx;
     const bool pbm = packed && c->pk.bm;   // brick-major packed words (dda.h)
@@ -3328,6 +3332,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             W.test_min = test_min;
             W.refill_min = refill_min;
             W.rel_min = rel ? rel_min : 0u;
+            W.rel_emin = rel_emin;
             W.esc = c->d_esc;
             for (uint32_t k = 0; k < nb; ++k) {
                 W.q_in = (k & 1) ? q0 : q1;
