@@ -120,6 +120,12 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #else
 #define ZRT_NORM_RN normalize
 #endif
+// the packed lane walk (primary, lane-walk bounces) skips a cell's refs that
+// the cell it left already tested (test_cell_keep), as the park kernel's test
+// rounds do
+#ifndef ZRT_WALK_FACE_SKIP
+#define ZRT_WALK_FACE_SKIP 1
+#endif
 // dda_init_fq (dda.h) in the primary / lane-walk wf_kernel too (the park
 // kernel's refill always takes it when ZRT_FAST_QUOT)
 #ifndef ZRT_FAST_QUOT_WF
@@ -293,6 +299,46 @@ __device__ __forceinline__ void test_cell(const TraceParams& p, uint32_t b, uint
     }
 }
 
+// test_cell for the packed walk's cells, with the entry-face skip of the
+// park kernel's test rounds (cell32_kernel): `keep` is the mask of the cell's
+// refs (bit k: ref b + k) still to test for the face the ray entered across,
+// all ones for a segment's first cell or cells above 32 refs.  A skipped ref
+// is bit-identical to one of the cell the ray just left, already tested
+// there, so the kept refs give the same nearest hit, in the same order.
+template <int TB, bool MTX>
+__device__ __forceinline__ void test_cell_keep(const TraceParams& p, uint32_t b, uint32_t e, uint32_t keep, v3 o,
+                                               v3 d, float& nearest, float& hu, float& hv, uint32_t& hidx) {
+    const uint32_t cnt = e - b;
+    if (cnt > 32u || keep == ~0u) {
+        uint32_t dummy = 0;
+        test_cell<TB, false, MTX>(p, b, e, o, d, nearest, hu, hv, hidx, dummy, nullptr);
+        return;
+    }
+    uint32_t m = keep & ((cnt < 32u ? (1u << cnt) : 0u) - 1u);
+    while (m) {
+        uint32_t k[TB];
+        bool has[TB];
+#pragma unroll
+        for (int j = 0; j < TB; ++j) {
+            has[j] = m != 0u;
+            k[j] = has[j] ? (uint32_t)__builtin_ctz(m) : k[0];
+            m &= m - 1u;
+        }
+        v3 A[TB], B[TB], Cc[TB];
+#pragma unroll
+        for (int j = 0; j < TB; ++j) load_tri(p, b + k[j], A[j], B[j], Cc[j]);
+#pragma unroll
+        for (int j = 0; j < TB; ++j) {
+            if (has[j]) {
+                float t, u, v;
+                if (tri_ray<MTX>(A[j], B[j], Cc[j], o, d, &t, &u, &v)) {
+                    if (nearest > t && t > 0.0f) { nearest = t; hu = u; hv = v; hidx = b + k[j]; }
+                }
+            }
+        }
+    }
+}
+
 // Scene.traceRay (stage3.zig:152-186) with empty-space skipping that changes
 // nothing in the result: the DDA arithmetic runs for every cell exactly as
 // Iterator.next does; only the 8-byte Cell load is skipped when the cell's
@@ -350,10 +396,27 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
         // bound) the t past which every cell of the ray is empty
         float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
+        // ZRT_WALK_FACE_SKIP: the crossing t of the step into the current
+        // cell (NaN: the segment's first tested cell, every ref tested)
+        float tcl = __builtin_nanf("");
         for (;;) {
             if (occupied) {
-                const uint2 cell = *reinterpret_cast<const uint2*>(p.cell32 + 8ull * s.pc);
-                test_cell<TB, false, MTX>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+                const uint32_t* rec = p.cell32 + 8ull * s.pc;
+                const uint2 cell = *reinterpret_cast<const uint2*>(rec);
+                if (ZRT_WALK_FACE_SKIP) {
+                    // the face entered: the stepped axis a is the one whose
+                    // next crossing is this step's own tc + td_a; exactly one
+                    // such axis, or (a tie at tc) every ref is tested
+                    const bool x0 = s.tn0 == tcl + s.td0, x1 = s.tn1 == tcl + s.td1, x2 = s.tn2 == tcl + s.td2;
+                    uint32_t keep = ~0u;
+                    if ((uint32_t)x0 + (uint32_t)x1 + (uint32_t)x2 == 1u) {
+                        const uint32_t face = x0 ? (s.d0 >> 31) : (x1 ? 2u + (s.d1 >> 31) : 4u + (s.d2 >> 31));
+                        keep = rec[2 + face];
+                    }
+                    test_cell_keep<TB, MTX>(p, cell.x, cell.y, keep, o, d, nearest, hu, hv, hidx);
+                } else {
+                    test_cell<TB, false, MTX>(p, cell.x, cell.y, o, d, nearest, hu, hv, hidx, n_tests, prof);
+                }
                 lim = fminf(lim, nearest);                 // = min(nearest, far bound)
             }
             bool crossed, exited;
@@ -362,6 +425,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             pkl.f0 = f0; pkl.f1 = f1; pkl.f2 = f2;
             DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
+            tcl = tc;
             if (crossed) occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
         }
         return nearest;
