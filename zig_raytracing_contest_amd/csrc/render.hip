@@ -122,9 +122,11 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #endif
 // the packed lane walk (primary, lane-walk bounces) skips a cell's refs that
 // the cell it left already tested (test_cell_keep), as the park kernel's test
-// rounds do
+// rounds do. Off: the primary holds 7 waves only with 6 VGPRs spilled, and
+// the r06aa A/B (profiles/r06/r06aa_ab_walk_face_skip.log) measured cfg3
+// -0.1%, cfg2 -0.3%, cfg5 -0.7% with it on (the primary's refs are few)
 #ifndef ZRT_WALK_FACE_SKIP
-#define ZRT_WALK_FACE_SKIP 1
+#define ZRT_WALK_FACE_SKIP 0
 #endif
 // dda_init_fq (dda.h) in the primary / lane-walk wf_kernel too (the park
 // kernel's refill always takes it when ZRT_FAST_QUOT)
