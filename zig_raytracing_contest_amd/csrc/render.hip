@@ -1094,6 +1094,19 @@ constexpr uint32_t kParkChunk = ZRT_PARK_CHUNK;
 #ifndef ZRT_PARK_LATE_DRAIN
 #define ZRT_PARK_LATE_DRAIN 1
 #endif
+// ZRT_PARK_QPF: at the end of a refill round the wave pulls the lines of the
+// next 64 queue entries of its chunk into L2 (one LDS-DMA dword per lane into
+// a per-wave scratch slot that nothing reads), so the next refill round's
+// record loads hit L2 instead of HBM.  The walk trips that follow do not wait
+// for vector memory; the next test round's vmcnt(0) is the first wait behind
+// the prefetch, and its ranges were issued after it.  Off: r06ab, 2 rounds,
+// images identical: cfg3 6972 vs 6992 (-0.3%), cfg2 -0.4%, cfg5 3845 vs 3892
+// (-1.2%) (profiles/r06/r06ab_ab_queue_prefetch.log): the extra request per
+// lane and refill costs more than the record loads' HBM latency, which the
+// SIMD's other park waves already hide
+#ifndef ZRT_PARK_QPF
+#define ZRT_PARK_QPF 0
+#endif
 // ZRT_PARK_ADAPT: a launch with few entries per wave (the last bounces, an
 // 8-rank tile set) takes smaller chunks, down to 64, so the waves' last
 // chunks end closer together (the launch tail).  r05e, alternating processes,
@@ -1239,6 +1252,10 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
     __shared__ uint32_t s_esc[kParkWaves * 64];             // escape-table words (park_load_esc)
     uint32_t* const esc_slot = s_esc + 64u * (threadIdx.x >> 6);
     __shared__ uint8_t s_sel8[256 * 8];                     // bit position of the r-th set bit of a byte
+#if ZRT_PARK_QPF
+    __shared__ uint32_t s_qpf[kParkWaves * 64];             // queue-record prefetch landing slots (never read)
+    uint32_t* const qpf_slot = s_qpf + 64u * (threadIdx.x >> 6);
+#endif
     for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) {
         SEL8_ENTRY(i, pos);
         s_sel8[i] = (uint8_t)pos;
@@ -1384,6 +1401,12 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
             // paths' record loads (vector memory completes in order); only a
             // round that loaded nothing drains them explicitly
             if (ZRT_PARK_LATE_DRAIN && !loaded) __builtin_amdgcn_s_waitcnt(0x3f70);
+#if ZRT_PARK_QPF
+            if (ce > cb) {
+                const uint32_t j = min(cb + lane, ce - 1u);
+                park_load_esc(reinterpret_cast<const uint32_t*>(w.q_in + 3ull * ent_index<false>(w, cgrp, j)), qpf_slot);
+            }
+#endif
             PARK_STAMP(0);
             if (__ballot(st != kIdle) == 0ull) {
                 if (!more) break;
@@ -1999,7 +2022,8 @@ constexpr uint32_t kLeadPct = ZRT_LEAD_PCT;
 constexpr size_t kParkSlotsBytes = (kParkBlock / 64) * sizeof(ParkSlot);
 constexpr size_t kOccxBudget = kLdsPerCu - kParkSlotsBytes - 514 * sizeof(double) - kParkWaves * 192 * 4 - 256 -
                                 256 * 8 -   // the select table
-                                kParkWaves * 64 * 4;   // the escape slots
+                                kParkWaves * 64 * 4 -  // the escape slots
+                                (ZRT_PARK_QPF ? kParkWaves * 64 * 4 : 0);   // the prefetch slots
 
 }  // namespace
 
