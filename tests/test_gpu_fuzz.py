@@ -164,6 +164,50 @@ def test_fuzz_scenes_cover_the_families():
     assert any(s.num_triangles >= 400 for s, *_ in draws)
 
 
+MEDIUM = list(range(12))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", MEDIUM)
+def test_fuzz_medium_scene_bitexact_vs_oracle(oracle_mod, seed):
+    """Larger draws (128-320 pixels a side, 4-16 spp, 2,000-20,000
+    triangles, 16-128 cells per axis): queues long enough for several park
+    chunks per wave, the two pass sets and multi-pass splits
+    (samples_per_pass); default, release forced on and the escape table forced
+    on, each equal to the oracle's whole frame."""
+    rng = np.random.default_rng(5000 + seed)
+    soup, _, _, _, _, _, rseed = _scene(seed + 10000)
+    n = int(rng.integers(2000, 20001))
+    pos = _triangles(rng, n)
+    v = pos.reshape(n, 3, 3)
+    fn = np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0])
+    fn = fn / np.maximum(np.linalg.norm(fn, axis=1, keepdims=True), 1e-20)
+    soup.pos = pos
+    soup.nrm = np.ascontiguousarray(np.repeat(fn, 3, axis=0).reshape(n, 9), F32)
+    soup.uv = np.ascontiguousarray(rng.uniform(-2, 3, (n, 6)), F32)
+    soup.mat = rng.integers(0, soup.num_materials, n).astype(np.uint32)
+    res = tuple(int(x) for x in rng.integers(16, 129, 3))
+    w, h = (int(x) for x in rng.integers(128, 321, 2))
+    spp = int(rng.integers(4, 17))
+    mb = int(rng.integers(1, 6))
+    c = soup.camera(None)
+    ocam = oracle_mod.camera_from_matrix(c.matrix, c.yfov, None, w, h)
+    rgb, lin, ctr = oracle_mod.OracleScene(soup, res).render(ocam, spp, mb, oracle_mod.RNG_PATH, rseed, 16)
+    cam = camera_for(soup, None, w, h)
+    pix = native.tile_pixels(cam.w, cam.h)
+    rs = RenderScene(soup, res, device_build=bool(seed % 2))
+    info = (seed, n, res, w, h, spp, mb)
+    try:
+        for flags, spp_pass in ((0, 0), (native.FLAG_RELEASE, 0), (native.FLAG_ESCAPE, 0), (0, max(1, spp // 3))):
+            fast, fo = rs.render(cam, num_samples=spp, max_bounce=mb, seed=rseed, linear=True, flags=flags,
+                                 samples_per_pass=spp_pass)
+            assert np.array_equal(fast.reshape(-1, 3), rgb), (flags, spp_pass) + info
+            assert np.array_equal(fo["linear"].view(np.uint32), lin[pix].view(np.uint32)), (flags, spp_pass) + info
+            assert fo["stats"]["segments"] == int(ctr[0]), (flags, spp_pass) + info
+    finally:
+        rs.close()
+
+
 @pytest.mark.gpu
 def test_fuzz_reached_every_bounce_kernel():
     """(runs after the scenes above) the draws rendered bounces through both

@@ -125,6 +125,16 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // rounds do. Off: the primary holds 7 waves only with 6 VGPRs spilled, and
 // the r06aa A/B (profiles/r06/r06aa_ab_walk_face_skip.log) measured cfg3
 // -0.1%, cfg2 -0.3%, cfg5 -0.7% with it on (the primary's refs are few)
+// ZRT_PRIMARY_BMASK: the packed lane walk (primary, lane-walk bounces) on
+// brick-major words reads, on entering an occupied brick, the brick's 64-bit
+// cell mask from global memory and loads a cell's record only when its own
+// bit is set.  With the brick bit alone every cell of an occupied brick cost
+// a dependent record load and an empty test: cfg3 camera rays walk 44 cells
+// after the frustum bound, 18.9 in occupied bricks, 4.2 non-empty (host
+// model, tools/frustum_sim.cpp on the bench scenes; cfg5 27.3 / 11.5 / 2.8)
+#ifndef ZRT_PRIMARY_BMASK
+#define ZRT_PRIMARY_BMASK 1
+#endif
 #ifndef ZRT_WALK_FACE_SKIP
 #define ZRT_WALK_FACE_SKIP 0
 #endif
@@ -166,6 +176,9 @@ struct TraceParams {
     const double* zig;        // zx[257], zf[257]
     const uint32_t* occ;      // brick occupancy bits (brick = 2^occ_shift cells per axis)
     uint32_t occ_shift, occ_nb0, occ_nb01, occ_words;
+    // per 4^3 brick in linear brick order (= pc >> 6 of a brick-major word)
+    // its 64-bit cell mask (occx_mask_kernel's), for the packed lane walk
+    const unsigned long long* bmask;
     // primary launch: per 8x8 pixel block of the image (row-major, tlo_nbx
     // blocks per row) the frustum bounds (lo, hi, unused, unused) of escape.h
     // frustum_bound, or null
@@ -395,6 +408,9 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             }
         }
         bool occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
+        constexpr bool kBm = PK_BM && ZRT_PRIMARY_BMASK;
+        unsigned long long q = 0ull;        // kBm: the current brick's cell mask
+        if (kBm && occupied) q = p.bmask[s.pc >> 6];
         // the walk's stop: the nearest hit so far, or (TFAR, a frustum far
         // bound) the t past which every cell of the ray is empty
         float lim = ZRT_FRUSTUM_HI && s0.neg < 8u ? tfar : kInf;
@@ -402,7 +418,7 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
         // cell (NaN: the segment's first tested cell, every ref tested)
         float tcl = __builtin_nanf("");
         for (;;) {
-            if (occupied) {
+            if (kBm ? ((q >> (s.pc & 63u)) & 1ull) != 0ull : occupied) {
                 const uint32_t* rec = p.cell32 + 8ull * s.pc;
                 const uint2 cell = *reinterpret_cast<const uint2*>(rec);
                 if (ZRT_WALK_FACE_SKIP) {
@@ -428,7 +444,10 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
             DDAV_STEPX(s, pkl, p.occ_lowm, crossed, exited, tc);
             if (exited || lim <= tc) break;                // stage3.zig:179-182 (T_EXIT = +inf at the exit)
             tcl = tc;
-            if (crossed) occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
+            if (crossed) {
+                occupied = brick_occupied_v<PK_BM>(p, occ, s.pc);
+                if (kBm) q = occupied ? p.bmask[s.pc >> 6] : 0ull;
+            }
         }
         return nearest;
     }
@@ -2048,6 +2067,7 @@ struct zrt_context {
     uint32_t* d_occ = nullptr;
     uint32_t occ_shift = 0, occ_nb[3] = {0, 0, 0}, occ_words = 0;
     uint32_t* d_occx = nullptr;     // exact per-cell occupancy blob (OccX), if it fits the LDS budget
+    unsigned long long* d_bmask = nullptr;   // every 4^3 brick's cell mask, linear brick order (TraceParams::bmask)
     uint32_t* d_esc = nullptr;      // escape table (escape.h), with OccX
     uint32_t* d_sat = nullptr;      // summed-area table of cell occupancy (escape.h EscSat), or null
     // the primary frustum bounds (frustum_kernel) per 8x8 pixel block
@@ -2240,7 +2260,7 @@ extern "C" void zrt_context_destroy(zrt_context* c) {
     DeviceGuard g(c->device);
     if (c->d_cell32) (void)hipFree(c->d_cell32);
     void* bufs[] = {c->d_cells, c->d_pos, c->d_data, c->d_mats, c->d_texels, c->d_zig, c->d_occ, c->d_occx, c->d_esc,
-                    c->d_sat, c->d_tlo,
+                    c->d_bmask, c->d_sat, c->d_tlo,
                     c->d_pix, c->d_out, c->d_acc, c->d_rgb, c->d_lin, c->d_counter, c->d_stats};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2427,7 +2447,8 @@ static int context_packed(zrt_context* c) {
     const uint32_t* r = c->grid.resolution;
     // brick-major words where the grid allows them and the primary's
     // occupancy bricks are 4^3 (it reads them by pc >> 6); else field words
-    c->packed = pack_layout(r, c->pk, ZRT_PACK_BM && c->occ_shift == 2u);
+    // (and the dense brick masks exist: trace_ray reads them by pc >> 6)
+    c->packed = pack_layout(r, c->pk, ZRT_PACK_BM && c->occ_shift == 2u && c->d_bmask != nullptr);
     if (!c->packed) return ZRT_OK;
     const uint64_t n = 1ull << (c->pk.b0 + c->pk.b1 + c->pk.b2);
     if (32 * n > kCell32Max || (n > 16ull * c->ncells && 32 * n > (1ull << 30))) {
@@ -2770,6 +2791,8 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
             if (rc != ZRT_OK) return rc;
             return context_counters(c);
         }
+        HIP_TRY(hipMalloc((void**)&c->d_bmask, nb * 8));
+        HIP_TRY(copy_sync(c->d_bmask, mask.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
         std::vector<uint32_t> bits(nbw, 0u);
         std::vector<uint16_t> prefix(nbw, 0);
         std::vector<unsigned long long> masks;
@@ -2808,19 +2831,17 @@ static int context_occupancy(zrt_context* c, const uint32_t* host_cells) {
         // the scratch buffers are freed on every exit path (the blob belongs
         // to the context as soon as it exists)
         struct Scratch {
-            unsigned long long* masks = nullptr;
             uint32_t* n = nullptr;
             ~Scratch() {
-                if (masks) (void)hipFree(masks);
                 if (n) (void)hipFree(n);
             }
         } tmp;
         uint32_t* d_blob = nullptr;
-        HIP_TRY(hipMalloc((void**)&tmp.masks, nb * 8));
+        HIP_TRY(hipMalloc((void**)&c->d_bmask, nb * 8));   // the dense masks stay (TraceParams::bmask)
         HIP_TRY(hipMalloc((void**)&tmp.n, 4));
         HIP_TRY(hipMalloc((void**)&d_blob, words * 4));
         c->d_occx = d_blob;            // freed with the context from here on
-        unsigned long long* const d_masks = tmp.masks;
+        unsigned long long* const d_masks = c->d_bmask;
         uint32_t* const d_n = tmp.n;
         HIP_TRY(hipMemsetAsync(d_blob, 0, words * 4, c->stream));
         hipLaunchKernelGGL(occx_mask_kernel, dim3((uint32_t)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
@@ -3317,6 +3338,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     tp.texels = c->d_texels;
     tp.zig = c->d_zig;
     tp.occ = c->d_occ;
+    tp.bmask = c->d_bmask;
     tp.occ_shift = c->occ_shift;
     tp.occ_nb0 = c->occ_nb[0];
     tp.occ_nb01 = c->occ_nb[0] * c->occ_nb[1];
