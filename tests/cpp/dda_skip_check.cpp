@@ -233,11 +233,17 @@ static void walk_ff(const GridK& k, const Dda& s0, std::mt19937_64& rng) {
             const float tmin = fminf(q.tn0, fminf(q.tn1, q.tn2));
             const float dmin = fminf(q.td0, fminf(q.td1, q.td2));
             const float tau = tmin + (float)(1 + rng() % 120) * dmin;
-            bool exited, exited4, exitedc;
-            DdaV x4 = x, xc = x;
+            bool exited, exited4, exitedc, exitedn;
+            DdaV x4 = x, xc = x, xn = x;
             DDAV_FF(x, pk.f0, pk.f1, pk.f2, tau, exited);
             DDAV_FF4(x4, pk.f0, pk.f1, pk.f2, tau, exited4);
             DDAV_FFC(xc, pk, pk.f0, pk.f1, pk.f2, tau, exitedc);
+            DDAV_FFN(xn, pk, pk.f0, pk.f1, pk.f2, tau, exitedn);
+            if (exitedn != exited || (!exited && (xn.pc != x.pc || memcmp(&xn.tn0, &x.tn0, 4) ||
+                                                  memcmp(&xn.tn1, &x.tn1, 4) || memcmp(&xn.tn2, &x.tn2, 4)))) {
+                ++g_ff_fails;
+                return;
+            }
             if (exited4 != exited || (!exited && (x4.pc != x.pc || memcmp(&x4.tn0, &x.tn0, 4) ||
                                                   memcmp(&x4.tn1, &x.tn1, 4) || memcmp(&x4.tn2, &x.tn2, 4)))) {
                 ++g_ff_fails;

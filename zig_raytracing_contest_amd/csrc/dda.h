@@ -385,6 +385,19 @@ ZHD uint32_t pack_coord(const PackK& k, uint32_t pc, int a) {
     if (k.bm) return ((pc >> (2 * a)) & 3u) | (((pc >> (a == 0 ? 6u : o)) & ((1u << (b - 2u)) - 1u)) << 2);
     return (pc >> o) & (b >= 32u ? ~0u : (1u << b) - 1u);
 }
+template <bool BM>
+ZHD uint32_t pack_coordt(const PackK& k, uint32_t pc, int a) {
+    const uint32_t o = a == 0 ? 0u : (a == 1 ? k.o1 : k.o2), b = a == 0 ? k.b0 : (a == 1 ? k.b1 : k.b2);
+    if (BM) return ((pc >> (2 * a)) & 3u) | (((pc >> (a == 0 ? 6u : o)) & ((1u << (b - 2u)) - 1u)) << 2);
+    return (pc >> o) & (b >= 32u ? ~0u : (1u << b) - 1u);
+}
+// The packed word with axis a's coordinate (field F) replaced by c
+template <bool BM>
+ZHD uint32_t pk_setc(const PackK& k, uint32_t pc, uint32_t f, int a, uint32_t c) {
+    const uint32_t o = a == 0 ? 0u : (a == 1 ? k.o1 : k.o2);
+    if (BM) return (pc & ~f) | ((c & 3u) << (2 * a)) | ((c >> 2) << (a == 0 ? 6u : o));
+    return (pc & ~f) | (c << o);
+}
 // pc + D on field F (D = +-lowbit(F), one cell): one add for contiguous
 // fields; for brick-major ones the gap between the field's two runs is filled
 // with ones (forward: the carry crosses it) or cleared (backward: the borrow
@@ -410,6 +423,8 @@ ZHD uint32_t pk_add(uint32_t pc, uint32_t f, uint32_t d) {
 #endif
     return ((g + d) & f) | (pc & ~f);
 }
+// (a masked add of n * D is NOT n steps on a brick-major field: n's bits
+// above the low run would land in the gap; pk_setc writes the coordinate)
 template <bool BM>
 ZHD uint32_t pk_addn(uint32_t pc, uint32_t f, uint32_t n, uint32_t d) {
     if (!BM) return pc + n * d;
@@ -705,6 +720,37 @@ ZHD uint32_t lm_selu(LaneM m, uint32_t t, uint32_t f) { return m ? t : f; }
         FF_AXIS4(S, 0, F0, TAU, EXITED)                                                        \
         if (!(EXITED)) { FF_AXIS4(S, 1, F1, TAU, EXITED) }                                     \
         if (!(EXITED)) { FF_AXIS4(S, 2, F2, TAU, EXITED) }                                     \
+    } while (0)
+
+// DDAV_FF with the packed cell stepped once per axis: per axis the crossings
+// below TAU as predicated f32 adds (four per loop trip) and their count n,
+// then the coordinate written once (pk_setc); EXITED when n reaches past the axis's exit
+// cell (FF_AXIS stops there: its crossing j is the exit one iff j - 1 cells
+// remained, so EXITED iff n > cells left).  The loop stops within four
+// crossings of n > left, so it runs at most left + 4 adds whatever TAU is.
+// Same crossings (the adds stop at the first t >= TAU), same state, same
+// EXITED as DDAV_FF; ~4 VALU per crossing instead of ~10.
+#define FFN_AXIS(S, K, A, FA, TAU, EXITED)                                                     \
+    {                                                                                          \
+        const uint32_t c_ = pack_coordt<PK_BM>((K), (S).pc, A), e_ = pack_coordt<PK_BM>((K), (S).pe, A); \
+        const uint32_t left_ = c_ > e_ ? c_ - e_ : e_ - c_;   /* cells before the exit one */  \
+        uint32_t n_ = 0;                                                                       \
+        while ((S).tn##A < (TAU) && n_ <= left_) {                                             \
+            _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                                 \
+                const bool go_ = (S).tn##A < (TAU);                                            \
+                (S).tn##A = go_ ? (S).tn##A + (S).td##A : (S).tn##A;                           \
+                n_ += go_ ? 1u : 0u;                                                           \
+            }                                                                                  \
+        }                                                                                      \
+        if (n_ > left_) (EXITED) = true;                                                       \
+        else (S).pc = pk_setc<PK_BM>((K), (S).pc, (FA), A, c_ > e_ ? c_ - n_ : c_ + n_);       \
+    }
+#define DDAV_FFN(S, K, F0, F1, F2, TAU, EXITED)                                                \
+    do {                                                                                       \
+        (EXITED) = false;                                                                      \
+        FFN_AXIS(S, K, 0, F0, TAU, EXITED)                                                     \
+        if (!(EXITED)) { FFN_AXIS(S, K, 1, F1, TAU, EXITED) }                                  \
+        if (!(EXITED)) { FFN_AXIS(S, K, 2, F2, TAU, EXITED) }                                  \
     } while (0)
 
 // DDAV_FF for long jumps: per axis first a run of n crossings known to lie

@@ -132,6 +132,13 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 // a dependent record load and an empty test: cfg3 camera rays walk 44 cells
 // after the frustum bound, 18.9 in occupied bricks, 4.2 non-empty (host
 // model, tools/frustum_sim.cpp on the bench scenes; cfg5 27.3 / 11.5 / 2.8)
+// ZRT_FFN: the frustum fast-forward as DDAV_FFN (dda.h: per axis predicated
+// adds and a count, the packed coordinate written once) instead of DDAV_FF4
+// (a packed step per crossing); cfg3 camera rays cross 85.6 cells below their
+// block's bound (tools/frustum_sim.cpp), cfg5 75.5, cfg2 62.8
+#ifndef ZRT_FFN
+#define ZRT_FFN 1
+#endif
 #ifndef ZRT_PRIMARY_BMASK
 #define ZRT_PRIMARY_BMASK 1
 #endif
@@ -403,7 +410,8 @@ __device__ __forceinline__ float trace_ray(const TraceParams& p, const uint32_t*
                 bool exited;
                 // (four branch-free crossings per loop trip: r04s, cfg3 5730 vs
                 // 5695 Mrays/s with one per trip, DDAV_FF)
-                DDAV_FF4(s, f0, f1, f2, tau, exited);
+                if (ZRT_FFN) DDAV_FFN(s, p.pk, f0, f1, f2, tau, exited);
+                else DDAV_FF4(s, f0, f1, f2, tau, exited);
                 if (exited) return nearest;
             }
         }
