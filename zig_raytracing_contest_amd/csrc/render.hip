@@ -120,18 +120,6 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #else
 #define ZRT_NORM_RN normalize
 #endif
-// the packed lane walk (primary, lane-walk bounces) skips a cell's refs that
-// the cell it left already tested (test_cell_keep), as the park kernel's test
-// rounds do. Off: the primary holds 7 waves only with 6 VGPRs spilled, and
-// the r06aa A/B (profiles/r06/r06aa_ab_walk_face_skip.log) measured cfg3
-// -0.1%, cfg2 -0.3%, cfg5 -0.7% with it on (the primary's refs are few)
-// ZRT_PRIMARY_BMASK: the packed lane walk (primary, lane-walk bounces) on
-// brick-major words reads, on entering an occupied brick, the brick's 64-bit
-// cell mask from global memory and loads a cell's record only when its own
-// bit is set.  With the brick bit alone every cell of an occupied brick cost
-// a dependent record load and an empty test: cfg3 camera rays walk 44 cells
-// after the frustum bound, 18.9 in occupied bricks, 4.2 non-empty (host
-// model, tools/frustum_sim.cpp on the bench scenes; cfg5 27.3 / 11.5 / 2.8)
 // ZRT_FFN: the frustum fast-forward as DDAV_FFN (dda.h: per axis predicated
 // adds and a count, the packed coordinate written once) instead of DDAV_FF4
 // (a packed step per crossing); cfg3 camera rays cross 85.6 cells below their
@@ -139,11 +127,25 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_FFN
 #define ZRT_FFN 1
 #endif
+// ZRT_PRIMARY_BMASK: the packed lane walk (primary, lane-walk bounces) on
+// brick-major words reads, on entering an occupied brick, the brick's 64-bit
+// cell mask from global memory and loads a cell's record only when its own
+// bit is set.  With the brick bit alone every cell of an occupied brick cost
+// a dependent record load and an empty test: cfg3 camera rays walk 44 cells
+// after the frustum bound, 18.9 in occupied bricks, 4.2 non-empty (host
+// model, tools/frustum_sim.cpp on the bench scenes; cfg5 27.3 / 11.5 / 2.8)
 #ifndef ZRT_PRIMARY_BMASK
 #define ZRT_PRIMARY_BMASK 1
 #endif
+// ZRT_WALK_FACE_SKIP: the packed lane walk (primary, lane-walk bounces) skips
+// a cell's refs that the cell it left already tested (test_cell_keep), as
+// the park kernel's test rounds do.  The r06aa A/B, before the exact cell
+// bits and the counted fast-forward, had it at -0.1% (cfg3); on the tree
+// after them (r06af, r06ag, 5 rounds) cfg3 +1.2%, cfg5 +0.3%, cfg2 +0.5%,
+// with 6 VGPRs of the 7-wave primary spilled outside its walk (6 waves: no
+// spill, cfg3 +0.9%)
 #ifndef ZRT_WALK_FACE_SKIP
-#define ZRT_WALK_FACE_SKIP 0
+#define ZRT_WALK_FACE_SKIP 1
 #endif
 // dda_init_fq (dda.h) in the primary / lane-walk wf_kernel too (the park
 // kernel's refill always takes it when ZRT_FAST_QUOT)
@@ -1959,9 +1961,13 @@ using WfFn = void (*)(const WfParams);
 // has no scratch access at all (12 at 7, 26 and walk reloads at 8).  Built
 // without SLP pairing (Makefile) the packed primary fits 7 waves (72 VGPRs,
 // no spill): r05ap, cfg3 6412 / 6400 vs 6346 / 6357 (+0.9%), cfg2 +0.7%,
-// cfg5 +0.3% (profiles/r05/r05ap_ab_primary7_select.log)
+// cfg5 +0.3% (profiles/r05/r05ap_ab_primary7_select.log).  Round 6: the
+// entry-face skip (ZRT_WALK_FACE_SKIP) spills 6-10 VGPRs at 7 waves, some in
+// the walk loop of the frustum instantiation; at 6 waves it spills nothing
+// and measured the same (r06af / r06ag: cfg3 +0.9 / +1.3% vs +1.3 / +1.2%
+// at 7 over the 7-wave tree without the skip)
 #ifndef ZRT_WF_MINW0
-#define ZRT_WF_MINW0 7
+#define ZRT_WF_MINW0 6
 #endif
 constexpr int kWfMinWaves = ZRT_WF_MINW;
 constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
