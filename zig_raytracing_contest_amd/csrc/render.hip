@@ -106,10 +106,6 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_FRUSTUM_HI
 #define ZRT_FRUSTUM_HI 1
 #endif
-// DDA steps per park walk trip, every cell's brick lookup in flight at once
-// (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
-// +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
-// primary frustum bounds per (1 << ZRT_FRUSTUM_SHIFT)^2 pixel block
 // the timed kernels' normalize: 1/length by recip_rn (zrt_math.h; the same
 // vector bit for bit)
 #ifndef ZRT_NORMALIZE_RN
@@ -152,8 +148,12 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #ifndef ZRT_FAST_QUOT_WF
 #define ZRT_FAST_QUOT_WF 1
 #endif
+// primary frustum bounds per (1 << ZRT_FRUSTUM_SHIFT)^2 pixel block: 4x4
+// since round 6, when the counted fast-forward (ZRT_FFN) made the crossings
+// below the bound cheap (r05ae had 8x8 = 4x4 = 2x2 at ~10 VALU per crossing);
+// r06ai / r06ak, 5 rounds: cfg3 +0.8 / +0.5%, cfg2 -0.3 / +0.1%, cfg5 0 / +0.1%
 #ifndef ZRT_FRUSTUM_SHIFT
-#define ZRT_FRUSTUM_SHIFT 3
+#define ZRT_FRUSTUM_SHIFT 2
 #endif
 constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
 // brick-major packed cell words for the grids that allow them (dda.h): r05ag,
@@ -165,6 +165,9 @@ constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
 #endif
 
 constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
+// DDA steps per park walk trip, every cell's brick lookup in flight at once
+// (r03h/r03i, full spp: 4 vs 2 cfg3 +2.6%, cfg5 +2.2%, cfg2 -0.2%; 6: cfg3
+// +0.4%, cfg5 +4.1%; 8: -8 to -10% everywhere)
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
@@ -188,7 +191,7 @@ struct TraceParams {
     // per 4^3 brick in linear brick order (= pc >> 6 of a brick-major word)
     // its 64-bit cell mask (occx_mask_kernel's), for the packed lane walk
     const unsigned long long* bmask;
-    // primary launch: per 8x8 pixel block of the image (row-major, tlo_nbx
+    // primary launch: per 2^kFrustShift-square pixel block of the image (row-major, tlo_nbx
     // blocks per row) the frustum bounds (lo, hi, unused, unused) of escape.h
     // frustum_bound, or null
     const float4* tlo;
@@ -3391,7 +3394,7 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (ZRT_FRUSTUM && c->d_sat && !counting && packed && !(cfg->flags & ZRT_FLAG_NO_FRUSTUM) &&
         ((uint64_t)P * cfg->num_samples >= kFrustumMinSamples || (cfg->flags & ZRT_FLAG_FRUSTUM))) {
         // the primary frustum bounds of this camera, every render (inside the
-        // timed region: 32 K threads for a 1080p frame)
+        // timed region: one wave per 4x4 pixel block, 130 K waves at 1080p)
         const uint32_t nbx = (cam->w + (1u << kFrustShift) - 1u) >> kFrustShift;
         const uint32_t nby = (cam->h + (1u << kFrustShift) - 1u) >> kFrustShift;
         if ((rc = grow(&c->d_tlo, &c->tlo_cap, (size_t)nbx * nby)) != ZRT_OK) return rc;
