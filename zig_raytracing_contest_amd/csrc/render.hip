@@ -1249,7 +1249,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x, uint32_t lane, uin
 // their activity (printed by zrt_context_render as zrt_park_profile; the
 // stamps cost ~10% and never run in the product build).
 #ifdef ZRT_SWEEP
-#define PARK_PROF_DECL unsigned long long pprof[20] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+#define PARK_PROF_DECL unsigned long long pprof[21] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     uint64_t ptick = __builtin_amdgcn_s_memtime();
 #define PARK_STAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pprof[k] += t_ - ptick; ptick = t_; } while (0)
 #define PARK_COUNT(k, v) (pprof[k] += (v))
@@ -1551,6 +1551,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
         // ---- test round: the parked lanes' cells, all pairs over all lanes
         if (__ballot(st == kPark) != 0ull) {
             __builtin_amdgcn_s_waitcnt(0x3f70);                    // vmcnt(0): the ranges landed
+            PARK_STAMP(20);                                        // (sweep: the round's wait for them)
             const bool ready = st == kPark;
             // the parked cell's refs still to test: those the mask keeps
             // (cells of at most 32 refs; larger ones test every ref)
@@ -1628,7 +1629,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
     if (lane == 0)
         for (int k = 0; k < 13; ++k) atomicAdd(&p.stats[16 + k], pprof[k]);
     if (lane == 0)
-        for (int k = 13; k < 20; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
+        for (int k = 13; k < 21; ++k) atomicAdd(&p.stats[48 + k - 13], pprof[k]);
 #endif
 }
 
@@ -3555,8 +3556,8 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
     if (getenv("ZRT_PARK_PROFILE") && park_next)
         fprintf(stderr, "{\"zrt_walk_steps\": {\"lane_steps\": %llu, \"empty_brick_steps\": %llu, "
                 "\"empty_brick_entries\": %llu, \"escapes\": %llu, \"parked_tested\": %llu, \"parked_no_refs\": %llu, "
-                "\"released_early\": %llu}}\n",
-                hs[48], hs[49], hs[50], hs[51], hs[52], hs[53], hs[54]);
+                "\"released_early\": %llu, \"cyc_round_wait\": %llu}}\n",
+                hs[48], hs[49], hs[50], hs[51], hs[52], hs[53], hs[54], hs[55]);
     if (getenv("ZRT_PARK_PROFILE") && !counting)
         fprintf(stderr, "{\"zrt_primary_profile\": {\"cyc_walk\": %llu, \"cyc_shade\": %llu, \"cyc_fetch_append\": %llu}}\n",
                 hs[29], hs[30], hs[31]);
