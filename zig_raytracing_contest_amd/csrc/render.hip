@@ -156,6 +156,7 @@ constexpr uint32_t kWfChunk = ZRT_WF_CHUNK;
 #define ZRT_FRUSTUM_SHIFT 2
 #endif
 constexpr uint32_t kFrustShift = ZRT_FRUSTUM_SHIFT;
+static_assert(kFrustShift <= 3, "a frustum block lies inside one tile (tile edges are multiples of 8)");
 // brick-major packed cell words for the grids that allow them (dda.h): r05ag,
 // 2 rounds, images identical: cfg3 6076 / 6088 vs 6005 / 5999 (+1.3%), cfg2
 // +2.4%, cfg5 +1.2%; the park walk trip 179 -> 165 VALU
@@ -2689,6 +2690,10 @@ struct FrustumArgs {
     uint32_t res[3];
     float bmin[3], bmax[3], cs[3], org[3], llc[3], right[3], up[3];
     uint32_t w, h, nbx, nby;
+    // this rank's tiles (capi.cpp tile_pixels: tile t of the tx-wide row-major
+    // grid belongs to rank t % nranks): tile edge in blocks, tiles per row,
+    // the rank and the rank count; the kernel bounds only their blocks
+    uint32_t tb, tx, rank, nranks;
 };
 __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
                                                          float4* __restrict__ tlo) {
@@ -2698,9 +2703,12 @@ __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restr
     // last occupied ones (a 1080p frame: 32 K waves of ~4 slices per lane
     // instead of 32 K threads of ~200 dependent slices, 0.42 ms, r04eb2)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t b = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    if (b >= a.nbx * a.nby) return;                        // (uniform over the wave)
-    const uint32_t bx = b % a.nbx, by = b / a.nbx;
+    // wave i: block i % tb^2 (row-major in the tile) of this rank's tile i / tb^2
+    const uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6, bpt = a.tb * a.tb;
+    const uint32_t t = a.rank + (i / bpt) * a.nranks, k = i % bpt;
+    const uint32_t bx = (t % a.tx) * a.tb + k % a.tb, by = (t / a.tx) * a.tb + k / a.tb;
+    if (bx >= a.nbx || by >= a.nby) return;                // (uniform over the wave)
+    const uint32_t b = by * a.nbx + bx;
     const FrustumCone q = frustum_cone(a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, kFrustB * bx,
                                        kFrustB * bx + kFrustB, kFrustB * by, kFrustB * by + kFrustB);
     int first = 1 << 30, last = -1;
@@ -3411,7 +3419,16 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
             fa.up[k] = cam->up[k];
         }
         fa.w = cam->w; fa.h = cam->h; fa.nbx = nbx; fa.nby = nby;
-        const uint64_t fthreads = (uint64_t)nbx * nby * 64u;
+        // only the blocks of this rank's tiles (a tile edge is a multiple of 8
+        // pixels, so of a block edge): an 8-rank frame bounds 1/8 of them
+        const uint32_t tile = cfg->tile_size ? cfg->tile_size : 64u;
+        fa.tb = tile >> kFrustShift;
+        fa.tx = (cam->w + tile - 1u) / tile;
+        fa.rank = cfg->rank;
+        fa.nranks = nranks;
+        const uint64_t ntiles = (uint64_t)fa.tx * ((cam->h + tile - 1u) / tile);
+        // (a rank with pixels owns tile `rank`, so ntiles > rank here)
+        const uint64_t fthreads = (ntiles - cfg->rank + nranks - 1u) / nranks * fa.tb * fa.tb * 64u;
         hipLaunchKernelGGL(frustum_kernel, dim3((uint32_t)((fthreads + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                            (const uint32_t*)c->d_sat, fa, c->d_tlo);
         HIP_TRY(hipGetLastError());
