@@ -172,6 +172,12 @@ constexpr double kFrustB = (double)(1u << ZRT_FRUSTUM_SHIFT);
 #ifndef ZRT_WALK_STEPS
 #define ZRT_WALK_STEPS 4
 #endif
+// the park kernel without the escape table (cfg2, cfg5) at 5 steps: r06ba, 2
+// rounds, cfg5 +0.55%, cfg2 +0.4%; with the table 5 steps spill in the walk
+// (cfg3 -6.7%) and 6 spill everywhere (cfg5 -8%)
+#ifndef ZRT_WALK_STEPS_NOESC
+#define ZRT_WALK_STEPS_NOESC 5
+#endif
 constexpr uint32_t kTriFloats = 12u;
 
 struct TraceParams {
@@ -1461,7 +1467,7 @@ __global__ __launch_bounds__(kParkBlock) ZRT_PARK_ATTR void wf_park_kernel(const
                 // select one v_cndmask on it (DDAV_STEPM: 179 VALU and no
                 // branch per four-step trip, against 202 VALU, 14 v_mov and
                 // four execz branches with per-lane booleans, r03p)
-                constexpr int kS = ZRT_WALK_STEPS;
+                constexpr int kS = ESC ? ZRT_WALK_STEPS : ZRT_WALK_STEPS_NOESC;
                 static_assert(kS >= 2, "the trip keeps the cell before its last step");
                 // the escape words landed so far (used at the trip's end, so the
                 // read's latency hides behind the trip)
