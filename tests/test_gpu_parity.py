@@ -561,6 +561,24 @@ def test_render_multipass_and_ranks_identical(gpu_scenes, mode, flags):
     assert np.array_equal(ref, img)
 
 
+@pytest.mark.parametrize("tile,nranks", [(32, 8), (8, 5), (64, 3)])
+def test_rank_tiles_with_frustum_bounds_identical(gpu_scenes, tile, nranks):
+    """Round 6: each rank bounds only its own tiles' frustum blocks
+    (FrustumArgs rank / nranks / tile).  Edge tiles cut by the image border,
+    tile edges of 8 (two 4x4 blocks) to 64 pixels: the ranks' images put
+    together equal the one-rank render with the bounds, and the counting build."""
+    soup = scenes.get_scene("cornell")
+    cam = camera_for(soup, None, 200, 120)
+    rs = gpu_scenes("cornell")
+    ref, _ = rs.render(cam, num_samples=3, max_bounce=4, stats=True)     # counting build: every cell walked
+    one, _ = rs.render(cam, num_samples=3, max_bounce=4, flags=native.FLAG_FRUSTUM)
+    assert np.array_equal(ref, one)
+    img = np.zeros_like(ref)
+    for r in range(nranks):
+        rs.context.render(cam, 3, 4, rank=r, num_ranks=nranks, tile=tile, image=img, flags=native.FLAG_FRUSTUM)
+    assert np.array_equal(ref, img)
+
+
 def test_two_stream_pass_sets_identical(gpu_scenes):
     """Passes alternate between two HIP streams with their own queues once a
     frame has 2^23 samples; the passes' sums into the accumulator must stay in
