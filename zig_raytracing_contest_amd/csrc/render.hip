@@ -54,9 +54,12 @@ constexpr int kBlock = 256;                          // resolve / probes / helpe
 constexpr int kTraceBlock = 512;                     // launch bound of wf_kernel / trace_kernel
 constexpr int kTraceThreads = 256;                   // threads per wf_kernel / trace_kernel block
 // (r03ze, full spp: 1 -1.3 / -0.6 / -1.5%, 3 -0.6 / -0.2 / -0.6% on cfg3 /
-// cfg2 / cfg5; 3 spills inside the primary's cell walk)
+// cfg2 / cfg5; 3 spills inside the primary's cell walk).  Round 6, with the
+// entry-face skip testing fewer refs per cell: 1 at 7 waves per SIMD (70
+// VGPRs, no spill) against 2 at 6 (r06bi + r06bj, 5 rounds): cfg3 +1.7 /
+// -0.05%, cfg2 +2.2 / +1.0%, cfg5 +0.35 / +0.5%; 1 at 6 waves: cfg3 -0.6%
 #ifndef ZRT_TRI_BATCH
-#define ZRT_TRI_BATCH 2
+#define ZRT_TRI_BATCH 1
 #endif
 constexpr int kTriBatch = ZRT_TRI_BATCH;             // triangle loads in flight per lane
 #ifndef ZRT_PARK_BLOCK_T
@@ -1976,9 +1979,11 @@ using WfFn = void (*)(const WfParams);
 // entry-face skip (ZRT_WALK_FACE_SKIP) spills 6-10 VGPRs at 7 waves, some in
 // the walk loop of the frustum instantiation; at 6 waves it spills nothing
 // and measured the same (r06af / r06ag: cfg3 +0.9 / +1.3% vs +1.3 / +1.2%
-// at 7 over the 7-wave tree without the skip)
+// at 7 over the 7-wave tree without the skip).  With one triangle load in
+// flight per lane (ZRT_TRI_BATCH 1) the primary fits 7 waves again (70
+// VGPRs, no spill): r06bi / r06bj
 #ifndef ZRT_WF_MINW0
-#define ZRT_WF_MINW0 6
+#define ZRT_WF_MINW0 7
 #endif
 constexpr int kWfMinWaves = ZRT_WF_MINW;
 constexpr int kWfMinWaves0 = ZRT_WF_MINW0;
