@@ -561,11 +561,12 @@ def test_render_multipass_and_ranks_identical(gpu_scenes, mode, flags):
     assert np.array_equal(ref, img)
 
 
-@pytest.mark.parametrize("tile,nranks", [(32, 8), (8, 5), (64, 3)])
+@pytest.mark.parametrize("tile,nranks", [(32, 8), (8, 5), (64, 3), (256, 2), (4096, 3)])
 def test_rank_tiles_with_frustum_bounds_identical(gpu_scenes, tile, nranks):
     """Round 6: each rank bounds only its own tiles' frustum blocks
     (FrustumArgs rank / nranks / tile).  Edge tiles cut by the image border,
-    tile edges of 8 (two 4x4 blocks) to 64 pixels: the ranks' images put
+    tile edges of 8 (two 4x4 blocks) to 4096 pixels (a tile larger than the
+    image: the kernel then filters the image's blocks by rank): the ranks' images put
     together equal the one-rank render with the bounds, and the counting build."""
     soup = scenes.get_scene("cornell")
     cam = camera_for(soup, None, 200, 120)

@@ -2703,8 +2703,10 @@ struct FrustumArgs {
     uint32_t w, h, nbx, nby;
     // this rank's tiles (capi.cpp tile_pixels: tile t of the tx-wide row-major
     // grid belongs to rank t % nranks): tile edge in blocks, tiles per row,
-    // the rank and the rank count; the kernel bounds only their blocks
-    uint32_t tb, tx, rank, nranks;
+    // the rank and the rank count; the kernel bounds only their blocks.
+    // whole: one wave per block of the image, those of other ranks' tiles
+    // leaving at once (tiles larger than the image: fewer waves that way)
+    uint32_t tb, tx, rank, nranks, whole;
 };
 __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restrict__ sat, const FrustumArgs a,
                                                          float4* __restrict__ tlo) {
@@ -2716,9 +2718,18 @@ __global__ __launch_bounds__(kBlock) void frustum_kernel(const uint32_t* __restr
     const uint32_t lane = threadIdx.x & 63u;
     // wave i: block i % tb^2 (row-major in the tile) of this rank's tile i / tb^2
     const uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6, bpt = a.tb * a.tb;
-    const uint32_t t = a.rank + (i / bpt) * a.nranks, k = i % bpt;
-    const uint32_t bx = (t % a.tx) * a.tb + k % a.tb, by = (t / a.tx) * a.tb + k / a.tb;
-    if (bx >= a.nbx || by >= a.nby) return;                // (uniform over the wave)
+    uint32_t bx, by;
+    if (a.whole) {                                         // (uniform over the wave)
+        if (i >= a.nbx * a.nby) return;
+        bx = i % a.nbx;
+        by = i / a.nbx;
+        if (((by / a.tb) * a.tx + bx / a.tb) % a.nranks != a.rank) return;
+    } else {
+        const uint32_t t = a.rank + (i / bpt) * a.nranks, k = i % bpt;
+        bx = (t % a.tx) * a.tb + k % a.tb;
+        by = (t / a.tx) * a.tb + k / a.tb;
+        if (bx >= a.nbx || by >= a.nby) return;
+    }
     const uint32_t b = by * a.nbx + bx;
     const FrustumCone q = frustum_cone(a.bmin, a.bmax, a.cs, a.org, a.llc, a.right, a.up, kFrustB * bx,
                                        kFrustB * bx + kFrustB, kFrustB * by, kFrustB * by + kFrustB);
@@ -3439,7 +3450,9 @@ extern "C" int zrt_context_render(zrt_context* c, const zrt_camera* cam, const z
         fa.nranks = nranks;
         const uint64_t ntiles = (uint64_t)fa.tx * ((cam->h + tile - 1u) / tile);
         // (a rank with pixels owns tile `rank`, so ntiles > rank here)
-        const uint64_t fthreads = (ntiles - cfg->rank + nranks - 1u) / nranks * fa.tb * fa.tb * 64u;
+        const uint64_t per_tile = (ntiles - cfg->rank + nranks - 1u) / nranks * fa.tb * fa.tb;
+        fa.whole = per_tile > (uint64_t)nbx * nby ? 1u : 0u;
+        const uint64_t fthreads = (fa.whole ? (uint64_t)nbx * nby : per_tile) * 64u;
         hipLaunchKernelGGL(frustum_kernel, dim3((uint32_t)((fthreads + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                            (const uint32_t*)c->d_sat, fa, c->d_tlo);
         HIP_TRY(hipGetLastError());
